@@ -1,0 +1,104 @@
+"""The CPU oracle against golden vectors produced by the reference itself
+(tests/golden/make_golden.py).  Schedule/timestep tables must match bit-exactly."""
+import numpy as np
+import pytest
+import torch
+
+from golden_util import load, cfg_of, weights_of
+from oracle import schedule as sch
+from oracle import unet_ref, vae_ref
+
+
+def test_register_schedule_bitexact():
+    z = load("schedule")
+    s = sch.register_schedule()
+    for k in ("betas", "alphas_cumprod", "alphas_cumprod_prev", "sqrt_one_minus_alphas_cumprod"):
+        assert s[k].dtype == z[k].dtype
+        assert np.array_equal(s[k].view(np.uint32), z[k].view(np.uint32)), k
+
+
+@pytest.mark.parametrize("S", [10, 50, 250])
+@pytest.mark.parametrize("eta", [0, 1])
+def test_ddim_tables_bitexact(S, eta):
+    z = load("schedule")
+    t = sch.ddim_tables(S, float(eta))
+    tag = f"S{S}_eta{eta}"
+    assert np.array_equal(t["ddim_timesteps"], z[tag + "_ts"])
+    assert t["ddim_timesteps"].dtype == np.int64
+    for mine, ref in (("ddim_alphas", "_alphas"), ("ddim_alphas_prev", "_alphas_prev"),
+                      ("ddim_sigmas", "_sigmas"), ("ddim_sqrt_one_minus_alphas", "_sqrt_one_minus")):
+        a, b = t[mine], z[tag + ref]
+        assert a.dtype == b.dtype, mine
+        assert np.array_equal(a, b), (mine, np.max(np.abs(a - b)))
+
+
+def test_ddim_uniform_50_timesteps():
+    ts = sch.make_ddim_timesteps("uniform", 50, 1000)
+    assert ts[0] == 1 and ts[-1] == 981 and len(ts) == 50 and np.all(np.diff(ts) == 20)
+
+
+@pytest.mark.parametrize("eta", [0, 1])
+@pytest.mark.parametrize("index", [0, 1, 25, 49])
+def test_ddim_step_bitexact(eta, index):
+    z = load("ddim_step")
+    tab = sch.ddim_tables(50, float(eta))
+    sc = sch.ddim_step_scalars(tab, index)
+    xp, p0 = sch.ddim_step(z["x"], z["e"], sc, noise=z["noise"] if eta else None)
+    ref_xp, ref_p0 = z[f"eta{eta}_i{index}_xprev"], z[f"eta{eta}_i{index}_pred_x0"]
+    assert np.array_equal(p0, ref_p0)
+    assert np.array_equal(xp, ref_xp), np.max(np.abs(xp - ref_xp))
+
+
+def test_timestep_embedding():
+    z = load("schedule")
+    t = torch.from_numpy(z["temb_t"])
+    assert np.array_equal(unet_ref.timestep_embedding(t, 320).numpy(), z["temb_320"])
+    assert np.array_equal(unet_ref.timestep_embedding(t, 33).numpy(), z["temb_33"])
+
+
+@pytest.mark.parametrize("name", ["unet_tiny", "unet_tiny_uncond", "unet_tiny_headch"])
+def test_unet_forward(name):
+    z = load(name)
+    cfg = cfg_of(z)
+    sd = weights_of(z)
+    ctx = torch.from_numpy(z["ctx"]) if "ctx" in z.files else None
+    y = unet_ref.unet_forward(sd, cfg, torch.from_numpy(z["x"]), torch.from_numpy(z["t"]), ctx)
+    ref = torch.from_numpy(z["y"])
+    err = (y - ref).abs().max().item()
+    assert err <= 1e-4 * max(1.0, ref.abs().max().item()), err
+
+
+def test_ddim_sampling_run():
+    """Full 4-step DDIM loop (ldm/diffusion/ddim.py ≡ DDIM/ddim.py) with the tiny UNet."""
+    from oracle.sampler_ref import ddim_sample
+    z = load("unet_tiny")
+    cfg, sd = cfg_of(z), weights_of(z)
+    ctx = torch.from_numpy(z["ctx"])
+    fn = lambda x, t: unet_ref.unet_forward(sd, cfg, x, t, ctx)
+    out, pred_x0 = ddim_sample(fn, torch.from_numpy(z["ddim_xT"]), int(z["ddim_steps"]), eta=0.0)
+    ref = z["ddim_samples"]
+    assert np.max(np.abs(out.numpy() - ref)) <= 1e-4 * max(1.0, np.abs(ref).max())
+
+
+def test_vae_decode():
+    z = load("vae_tiny")
+    cfg = cfg_of(z)
+    sd = weights_of(z)
+    dec = vae_ref.decode_first_stage(sd, cfg, torch.from_numpy(z["z"]), float(z["scale_factor"]))
+    ref = z["dec"]
+    assert np.max(np.abs(dec.numpy() - ref)) <= 1e-4 * max(1.0, np.abs(ref).max())
+
+
+def test_ddpm_c1_pipeline():
+    z = load("ddpm_c1")
+    tab = sch.ddpm_tables(1e-4, 1e-2, 10)
+    for k in ("betas", "alphas", "alphas_hat"):
+        assert np.array_equal(tab[k], z[k]), k
+    img = z["x0"]
+    noises = list(z["noises"])
+    for t in range(9, -1, -1):
+        ts = np.full((img.shape[0],), t, dtype=np.float32)
+        eps = (np.float32(0.5) * img + np.float32(0.01) * ts[:, None, None, None]).astype(np.float32)
+        sc = sch.ddpm_step_scalars(tab, t)
+        img = sch.ddpm_step(img, eps, sc, noises.pop(0) if t > 0 else None)
+    assert np.max(np.abs(img - z["out"])) <= 1e-5 * max(1.0, np.abs(z["out"]).max())
