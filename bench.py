@@ -1,0 +1,261 @@
+"""Headline benchmark: SD-1.x txt2img, 512x512, 50-step DDIM + VAE decode (BASELINE.json config C3/C4).
+
+One "step" = one full pass of the hot path over one batch: DDIM sampling (50
+UNet evaluations + 50 fused DDIM updates) of B latents 4x64x64 with a 77x768
+context, then the KL-VAE decode to B images 3x512x512.  Weights are seeded
+random (SD-1.x architecture, 860M UNet + 83.7M VAE); inputs are synthetic.
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
+one process per GPU; the latents of a global batch N*B are generated on the
+host from one seed and sliced per rank (weak scaling: B per GPU); no per-step
+collective; one RCCL all_gather_into_tensor of the decoded images at the end of
+every step.  Timing: barrier + synchronize on both sides of the K timed steps,
+max over ranks.  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+PEAK_F16_TFLOPS = 2500.0        # MI355X dense fp16/bf16 MFMA (MI355X_MICROARCH.md, no sparsity)
+PEAK_HBM_GBS = 8000.0
+
+SD1_UNET = dict(image_size=32, in_channels=4, out_channels=4, model_channels=320, attention_resolutions=[4, 2, 1],
+                num_res_blocks=2, channel_mult=[1, 2, 4, 4], num_heads=8, use_spatial_transformer=True,
+                transformer_depth=1, context_dim=768, use_checkpoint=False, legacy=False)
+SD_VAE = dict(double_z=True, z_channels=4, resolution=256, in_channels=3, out_ch=3, ch=128, ch_mult=[1, 2, 4, 4],
+              num_res_blocks=2, attn_resolutions=[], dropout=0.0)
+CONFIGS = {
+    "c3": dict(workload="sd1-txt2img-512-ddim50", unet=SD1_UNET, latent=64, ctx=(77, 768), batch=16),
+    "c2": dict(workload="ldm-uncond-256-ddim50", unet=dict(SD1_UNET, use_spatial_transformer=False,
+                                                           context_dim=None), latent=32, ctx=None, batch=8),
+    "c5": dict(workload="sd2shape-768-vpred-ddim50", unet=dict(SD1_UNET, num_heads=-1, num_head_channels=64,
+                                                               context_dim=1024), latent=96, ctx=(77, 1024),
+               batch=8, v=True),
+}
+
+
+def synth_init_(module, seed, device):
+    """Seeded N(0, 0.02^2) conv/linear weights (zero-init layers included), zero biases,
+    GN/LN gamma=1 beta=0 — SURVEY §8(d) synthetic weights, materialised on the device."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    for name, p in module.named_parameters():
+        if p.dim() >= 2:
+            p.data = torch.randn(p.shape, generator=g, device=device) * 0.02
+        elif name.endswith("bias"):
+            p.data = torch.zeros(p.shape, device=device)
+        else:
+            p.data = torch.ones(p.shape, device=device)
+
+
+def build_models(cfg, device):
+    import sd_amd_loader
+    sd_amd_loader.load()
+    from sd_amd.openai_model.model import UNetModel
+    from sd_amd.VAE.autoencoder import AutoEncoderKL
+    from sd_amd.DDIM.diffusion_modules import register_schedule
+    with torch.device("meta"):
+        unet = UNetModel(**cfg["unet"])
+        vae = AutoEncoderKL(ddconfig=SD_VAE, embed_dim=4)
+    unet = unet.to_empty(device=device)
+    vae = vae.to_empty(device=device)
+    synth_init_(unet, 1234, device)
+    synth_init_(vae, 4321, device)
+    unet.prepare(device)
+    vae.prepare(device)
+    sch = register_schedule(1000, 0.00085, 0.012)
+
+    class LatentModel:
+        """LatentDiffusion.apply_model / decode_first_stage semantics (Diffusion/ddpm.py)."""
+        num_timesteps = 1000
+        alphas_cumprod = sch["alphas_cumprod"]
+        parameterization = "v" if cfg.get("v") else "eps"
+        scale_factor = 0.18215
+
+        def __init__(self):
+            self.device = device
+
+        def apply_model(self, x, t, c):
+            return unet(x, t, context=c)
+
+        def decode_first_stage(self, z):
+            return vae.decode(z, pre_scale=1.0 / self.scale_factor)
+
+    return unet, vae, LatentModel()
+
+
+def unet_gflops_per_image(cfg):
+    return {"c3": 803.3, "c2": 125.1, "c5": 2149.1}[cfg]
+
+
+def vae_gflops_per_image(cfg):
+    return {"c3": 2514.5, "c2": 622.2, "c5": 5754.3}[cfg]
+
+
+def cpu_baseline(cfg_name, cfg, ddim_steps, threads):
+    """The fp32 CPU oracle (a port of the reference path) timed on this host: one UNet
+    evaluation + one VAE decode at batch 1, extrapolated to a full 50-step image."""
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from oracle.unet_ref import unet_forward
+    from oracle.vae_ref import decode_first_stage
+    from sd_amd.openai_model.model import UNetModel
+    from sd_amd.VAE.autoencoder import AutoEncoderKL
+    torch.set_num_threads(threads)
+    with torch.device("meta"):
+        um = UNetModel(**cfg["unet"])
+        vm = AutoEncoderKL(ddconfig=SD_VAE, embed_dim=4)
+    g = torch.Generator().manual_seed(0)
+    usd = {k: torch.randn(v.shape, generator=g) * 0.02 if v.dim() >= 2 else torch.zeros(v.shape)
+           for k, v in um.state_dict().items()}
+    vsd = {k: torch.randn(v.shape, generator=g) * 0.02 if v.dim() >= 2 else torch.ones(v.shape)
+           for k, v in vm.state_dict().items()}
+    L = cfg["latent"]
+    x = torch.randn(1, 4, L, L, generator=g)
+    ctx = torch.randn(1, *cfg["ctx"], generator=g) if cfg["ctx"] else None
+    t0 = time.perf_counter()
+    unet_forward(usd, cfg["unet"], x, torch.tensor([501]), ctx)
+    t_unet = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    decode_first_stage(vsd, SD_VAE, x, 0.18215)
+    t_vae = time.perf_counter() - t0
+    per_img = ddim_steps * t_unet + t_vae
+    return {"value": 1.0 / per_img, "unit": "images/sec", "cores": threads, "kind": "port",
+            "sample": f"fp32 CPU oracle: 1 UNet eval ({t_unet:.2f} s) + 1 VAE decode ({t_vae:.2f} s) at batch 1, "
+                      f"{L}x{L} latent, extrapolated to {ddim_steps} DDIM steps + decode per image"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the config's)")
+    ap.add_argument("--ddim-steps", type=int, default=50)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-roofline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local if dist else 0)
+    torch.cuda.set_device(device)
+    cfg = CONFIGS[args.config]
+    B = args.batch or cfg["batch"]
+    L = cfg["latent"]
+
+    unet, vae, model = build_models(cfg, device)
+    from sd_amd.DDIM.ddim import DDIMSampler
+    from sd_amd import ops
+    sampler = DDIMSampler(model)
+
+    # host-generated global batch, sliced per rank (parity with any rank count)
+    g = torch.Generator().manual_seed(2024)
+    xT_all = torch.randn(world * B, 4, L, L, generator=g)
+    ctx_all = torch.randn(world * B, *cfg["ctx"], generator=g) if cfg["ctx"] else None
+    xT = xT_all[rank * B:(rank + 1) * B].to(device)
+    ctx = ctx_all[rank * B:(rank + 1) * B].to(device) if ctx_all is not None else None
+    gathered = torch.empty(world * B, 3, 8 * L, 8 * L, dtype=torch.float16, device=device) if dist else None
+
+    def one_step():
+        z, _ = sampler.sample(S=args.ddim_steps, batch_size=B, shape=(4, L, L), conditioning=ctx, eta=0.0, x_T=xT,
+                              verbose=False, log_every_t=10 ** 9)
+        img = model.decode_first_stage(z)
+        if dist:
+            import torch.distributed as tdist
+            tdist.all_gather_into_tensor(gathered, img.half())
+        return img
+
+    def barrier():
+        if dist:
+            import torch.distributed as tdist
+            tdist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        one_step()
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        if i == args.steps - 1 and not args.no_roofline:
+            ops.PROFILER.start()
+        img = one_step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    ops.PROFILER.stop()
+    if dist:
+        import torch.distributed as tdist
+        tt = torch.tensor([elapsed], device=device)
+        tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+        elapsed = tt.item()
+    finite = bool(torch.isfinite(img).all().item())
+
+    # UNet step latency at the config batch (HIP events around one forward)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    tts = torch.full((B,), 501, dtype=torch.long, device=device)
+    unet(xT, tts, ctx)
+    torch.cuda.synchronize()
+    e0.record()
+    nrep = 5
+    for _ in range(nrep):
+        unet(xT, tts, ctx)
+    e1.record()
+    torch.cuda.synchronize()
+    unet_ms = e0.elapsed_time(e1) / nrep
+
+    images = world * B * args.steps
+    value = images / elapsed
+    out = {"metric": METRIC, "value": round(value, 4), "unit": "images/sec", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 2), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "f16", "data": "synthetic (seeded random weights, "
+           "N(0,1) latents, N(0,1) 77-token context)",
+           "config": {"workload": cfg["workload"], "global_batch": world * B, "batch_per_gpu": B,
+                      "latent": [4, L, L], "image": [3, 8 * L, 8 * L], "ddim_steps": args.ddim_steps, "eta": 0.0,
+                      "parallelism": f"dp{world}", "collective": "all_gather decoded images (RCCL)" if dist else None},
+           "unet_step_ms": round(unet_ms, 3), "finite": finite}
+    if not args.no_roofline and rank == 0:
+        summ = ops.PROFILER.summary()
+        conv = {"launches": 0, "ms": 0.0, "flops": 0.0}
+        for k, d in summ.items():
+            if k.startswith("conv"):
+                for f in conv:
+                    conv[f] += d[f]
+        if conv["launches"]:
+            avg_s = conv["ms"] / 1000.0 / conv["launches"]
+            ach = conv["flops"] / conv["launches"] / avg_s / 1e12
+            out["roofline"] = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
+                               "frac": round(ach / PEAK_F16_TFLOPS, 4), "traffic": None,
+                               "kernel": "conv_igemm_kernel (+splitk_reduce_kernel on split-K launches)",
+                               "launches": conv["launches"], "avg_launch_us": round(1e6 * avg_s, 2),
+                               "flops_per_launch": conv["flops"] / conv["launches"]}
+        out["kernel_time_ms_last_step"] = {k: round(v["ms"], 2) for k, v in summ.items()}
+        tot_tf = (unet_gflops_per_image(args.config) * args.ddim_steps + vae_gflops_per_image(args.config)) / 1000
+        out["end_to_end_tflops"] = round(tot_tf * value, 1)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.config, cfg, args.ddim_steps, args.cpu_threads)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        import torch.distributed as tdist
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,195 @@
+/*
+ * sdk_amd.h — C ABI of the MI355X (gfx950) latent-diffusion hot path.
+ *
+ * The reference (ProgramerSalar/stable-diffusion-from-scratch) has no FFI: its
+ * hot path is a chain of stock torch.nn ops plus two un-vendored flash_attn
+ * entry points.  Each entry point below replaces a family of those call sites
+ * (cited per function, file:line into the reference).  The library is driven
+ * by the Python mirror of the reference's modules (UNetModel, AutoEncoderKL,
+ * DDIMSampler) in stable-diffusion-from-scratch_amd/ through ctypes.
+ *
+ * Conventions (all entry points):
+ *   - activations are NHWC (token-major) IEEE fp16; statistics and the sampler
+ *     state are fp32; every pointer is device memory owned by the caller;
+ *   - the library allocates nothing per call; work launches on `stream`
+ *     (a hipStream_t, NULL = legacy default) and never synchronises, so a
+ *     caller may capture the calls into a hipGraph;
+ *   - return 0 on success or a negative sdk_status; sdk_last_error() returns a
+ *     thread-local message for the last failure.
+ */
+#ifndef SDK_AMD_H
+#define SDK_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* sdk_stream_t;
+
+enum sdk_status {
+  SDK_OK = 0,
+  SDK_EINVAL = -1,      /* bad shape / pointer / alignment */
+  SDK_EHIP = -2,        /* HIP launch error */
+  SDK_EWORKSPACE = -3   /* workspace too small */
+};
+
+/* ---------------------------------------------------------------- convolution / GEMM
+ * Implicit-GEMM convolution on MFMA (v_mfma_f32_32x32x16_f16, fp32 accumulate).
+ * out[m, n] = sum_k A[m, k] * W[n, k]  (+ bias[n] + row_bias[b(m), n]) (+ residual[m, n])
+ * where A is the im2col view of up to two K segments.  Each segment reads one
+ * or two NHWC sources (a channel concat, zero-copy), optionally through a
+ * GroupNorm affine (per (batch, channel) scale/shift) and SiLU, optionally
+ * nearest-x2 upsampled, with zero padding applied AFTER the transform.
+ * A plain Linear on tokens is the 1x1 case with h = tokens, w = 1.
+ *
+ * Replaces: nn.Conv2d 3x3/1x1/s2 (openai_model/utils.py:26-39 via model.py:117,181,207,218,365,531,88-90;
+ *   Unet/unet.py:84-112; Encoder_Decoder/encoder.py:133,171), nn.Linear
+ *   (openai_model/attention.py:40-47,133,164-168; model.py:197-200,352-357), the
+ *   GroupNorm32/Normalize + SiLU in front of them (openai_model/utils.py:15-22,
+ *   attention.py:10-11, Unet/unet.py:9-28), F.interpolate nearest x2 (model.py:127,
+ *   Unet/unet.py:46), torch.cat skip concat (model.py:586), the emb broadcast add
+ *   (model.py:241-250), the residual adds (model.py:252, attention.py:251-253,363,
+ *   Unet/unet.py:135, Unet/attention.py:264) and GEGLU x*gelu(gate) (attention.py:140-141).
+ */
+typedef struct {
+  const void* src0;        /* NHWC fp16, channels [0, c_split) */
+  const void* src1;        /* NHWC fp16, channels [c_split, cin) (NULL if c_split == cin) */
+  int32_t c_split;         /* multiple of 8 */
+  int32_t cin;             /* multiple of 8 */
+  int32_t ld0, ld1;        /* elements between consecutive pixels of src0 / src1 */
+  int32_t h, w;            /* source spatial size (before upsampling) */
+  int32_t ksize;           /* 1 or 3 */
+  int32_t stride, pad;
+  int32_t upsample;        /* 1: source is read nearest-x2 upsampled (logical 2h x 2w) */
+  const float* gn_scale;   /* [batch][cin] or NULL */
+  const float* gn_shift;   /* [batch][cin] or NULL */
+  int32_t silu;            /* apply x*sigmoid(x) after the affine */
+} sdk_conv_src;
+
+enum sdk_out_mode {
+  SDK_OUT_NHWC_F16 = 0,    /* out[m*out_ld + n] fp16 */
+  SDK_OUT_NCHW_F32 = 1,    /* out[(b*cout + n)*ho*wo + pix] fp32 */
+  SDK_OUT_GEGLU_F16 = 2,   /* weight rows packed in 32-row (x, gate) pairs; out width cout/2 */
+  SDK_OUT_ROWS_F32 = 3     /* out[m*out_ld + n] fp32 */
+};
+
+typedef struct {
+  int32_t batch, ho, wo, cout;
+  int32_t nseg;            /* 1 or 2 (segment 1 = fused 1x1 shortcut) */
+  sdk_conv_src seg[2];
+  const void* weight;      /* fp16 [cout_pad][k_total]; cout_pad = roundup(cout, 128);
+                              per segment: taps x roundup(cin, 64) columns, tap-major */
+  int32_t k_total;
+  const float* bias;       /* [cout] or NULL */
+  const float* row_bias;   /* [batch][row_bias_ld] or NULL (timestep-embedding broadcast) */
+  int32_t row_bias_ld;
+  const void* residual;    /* fp16 [M][res_ld] or NULL */
+  int32_t res_ld;
+  void* out;
+  int32_t out_ld;
+  int32_t out_mode;        /* enum sdk_out_mode */
+  int32_t split_k;         /* 0 = choose; 1 = off */
+  float* workspace;        /* split-K fp32 partials */
+  int64_t workspace_bytes;
+} sdk_conv_args;
+
+typedef struct {
+  int32_t split_k;
+  int32_t grid_tiles;
+  int64_t workspace_bytes;
+  int32_t variant;         /* kernel variant id (index into sdk_kernel_name) */
+  double flops;            /* algorithmic 2*M*N*K over the unpadded K */
+} sdk_conv_plan_info;
+
+int sdk_conv2d_plan(const sdk_conv_args* a, sdk_conv_plan_info* info);
+int sdk_conv2d(const sdk_conv_args* a, sdk_stream_t stream);
+
+/* ---------------------------------------------------------------- GroupNorm statistics
+ * Per (batch, group) mean / variance over an NHWC tensor (optionally a 2-source
+ * channel concat), folded with gamma/beta into per (batch, channel)
+ * scale = gamma*rstd, shift = beta - mean*gamma*rstd consumed by sdk_conv2d.
+ * Replaces the statistics half of GroupNorm32 (openai_model/utils.py:15-22, eps 1e-5),
+ * Normalize (openai_model/attention.py:10-11; Unet/unet.py:9-19, eps 1e-6) and
+ * FlashAttentionBlock.norm (Unet/attention.py:231, eps 1e-5).
+ */
+typedef struct {
+  const void* src0; const void* src1;
+  int32_t c_split, ld0, ld1;
+  int32_t batch, hw, channels, groups;
+  float eps;
+  const float* gamma; const float* beta;   /* [channels] */
+  float* scale; float* shift;              /* [batch][channels] */
+  float* workspace; int64_t workspace_bytes;
+} sdk_group_norm_args;
+
+int64_t sdk_group_norm_workspace(int32_t batch, int32_t hw, int32_t channels);
+int sdk_group_norm_affine(const sdk_group_norm_args* a, sdk_stream_t stream);
+
+/* ---------------------------------------------------------------- LayerNorm
+ * y = (x - mean) * rstd * gamma + beta over the last dim, fp16 in/out, fp32 math.
+ * Replaces nn.LayerNorm norm1/2/3 (openai_model/attention.py:216-218,251-253).
+ */
+int sdk_layer_norm(const void* x, void* y, int32_t rows, int32_t cols, int32_t ld_x, int32_t ld_y,
+                   const float* gamma, const float* beta, float eps, sdk_stream_t stream);
+
+/* ---------------------------------------------------------------- attention
+ * O = softmax(scale * Q K^T) V per (batch, head), non-causal, fp16 in/out, fp32
+ * softmax; flash-style (online softmax, scores never leave the CU).
+ * q/k/v/o are token-major: element (b, token, head, d) at ptr[(b*n + token)*ld + head*head_dim + d].
+ * Replaces flash_attn_func (openai_model/attention.py:106-112; Unet/attention.py:257)
+ * and flash_attn_qkvpacked_func (openai_model/attention.py:389-394,516-521).
+ */
+typedef struct {
+  const void* q; const void* k; const void* v; void* o;
+  int32_t q_ld, k_ld, v_ld, o_ld;
+  int32_t batch, heads, nq, nk, head_dim;
+  float scale;
+} sdk_attention_args;
+
+int sdk_attention(const sdk_attention_args* a, sdk_stream_t stream);
+
+/* ---------------------------------------------------------------- sampler / glue
+ * DDIM update (DDIM/ddim.py:194-204 == ldm/diffusion/ddim.py:197-205), fp32,
+ * evaluated op by op without contraction so it is bit-identical to torch's CPU
+ * kernels on the same inputs.  Optional fused classifier-free guidance
+ * (ddim.py:171-178: e = e_u + g*(e_c - e_u)) and v-prediction (extension: e =
+ * sqrt(a)*v + sqrt(1-a)*x).
+ */
+typedef struct {
+  const float* x; const float* e; const float* e_uncond; const float* noise;
+  float* x_prev; float* pred_x0;
+  int64_t n;
+  float sqrt_one_minus_at, sqrt_at, dir_coef, sqrt_a_prev, sigma, temperature;
+  float guidance;          /* used when e_uncond != NULL */
+  int32_t v_param;         /* 1: e holds v; convert with v_sqrt_a / v_sqrt_1ma */
+  float v_sqrt_a, v_sqrt_1ma;
+} sdk_ddim_args;
+
+int sdk_ddim_step(const sdk_ddim_args* a, sdk_stream_t stream);
+
+/* DDPM ancestral update (DDPM/ddpm.py:84-86):
+ * x = inv_sqrt_alpha*(x - coef*eps) + sigma*noise. */
+int sdk_ddpm_step(const float* x, const float* eps, const float* noise, float* out, int64_t n,
+                  float inv_sqrt_alpha, float coef, float sigma, sdk_stream_t stream);
+
+/* Sinusoidal timestep embedding cat[cos(t*f), sin(t*f)] -> fp16 (openai_model/utils.py:225-245;
+ * the reference feeds time_embed with t_emb.half(), model.py:566). */
+int sdk_timestep_embedding(const int64_t* t, const float* freqs, void* out, int32_t batch, int32_t dim,
+                           sdk_stream_t stream);
+
+/* NCHW fp32 -> NHWC fp16 with channel zero-padding to c_pad and a scalar pre-scale
+ * (x.type(dtype), model.py:572; 1/scale_factor*z, ldm/diffusion/ddpm.py:1095). */
+int sdk_nchw_to_nhwc(const float* x, void* y, int32_t batch, int32_t channels, int32_t hw, int32_t c_pad,
+                     float scale, sdk_stream_t stream);
+
+/* ---------------------------------------------------------------- introspection */
+const char* sdk_last_error(void);
+int sdk_version(void);
+const char* sdk_kernel_name(int32_t variant);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SDK_AMD_H */

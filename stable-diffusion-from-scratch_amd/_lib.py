@@ -1,0 +1,97 @@
+"""ctypes binding of libsdk_amd.so — the C ABI declared in include/sdk_amd.h.
+
+No fallback: if the library is missing or fails to load, every op raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsdk_amd.so")
+
+vp = C.c_void_p
+i32 = C.c_int32
+i64 = C.c_int64
+f32 = C.c_float
+fp = C.POINTER(C.c_float)
+
+
+class ConvSrc(C.Structure):
+    _fields_ = [("src0", vp), ("src1", vp), ("c_split", i32), ("cin", i32), ("ld0", i32), ("ld1", i32),
+                ("h", i32), ("w", i32), ("ksize", i32), ("stride", i32), ("pad", i32), ("upsample", i32),
+                ("gn_scale", vp), ("gn_shift", vp), ("silu", i32)]
+
+
+class ConvArgs(C.Structure):
+    _fields_ = [("batch", i32), ("ho", i32), ("wo", i32), ("cout", i32), ("nseg", i32), ("seg", ConvSrc * 2),
+                ("weight", vp), ("k_total", i32), ("bias", vp), ("row_bias", vp), ("row_bias_ld", i32),
+                ("residual", vp), ("res_ld", i32), ("out", vp), ("out_ld", i32), ("out_mode", i32),
+                ("split_k", i32), ("workspace", vp), ("workspace_bytes", i64)]
+
+
+class ConvPlanInfo(C.Structure):
+    _fields_ = [("split_k", i32), ("grid_tiles", i32), ("workspace_bytes", i64), ("variant", i32),
+                ("flops", C.c_double)]
+
+
+class GroupNormArgs(C.Structure):
+    _fields_ = [("src0", vp), ("src1", vp), ("c_split", i32), ("ld0", i32), ("ld1", i32), ("batch", i32),
+                ("hw", i32), ("channels", i32), ("groups", i32), ("eps", f32), ("gamma", vp), ("beta", vp),
+                ("scale", vp), ("shift", vp), ("workspace", vp), ("workspace_bytes", i64)]
+
+
+class AttentionArgs(C.Structure):
+    _fields_ = [("q", vp), ("k", vp), ("v", vp), ("o", vp), ("q_ld", i32), ("k_ld", i32), ("v_ld", i32),
+                ("o_ld", i32), ("batch", i32), ("heads", i32), ("nq", i32), ("nk", i32), ("head_dim", i32),
+                ("scale", f32)]
+
+
+class DdimArgs(C.Structure):
+    _fields_ = [("x", vp), ("e", vp), ("e_uncond", vp), ("noise", vp), ("x_prev", vp), ("pred_x0", vp),
+                ("n", i64), ("sqrt_one_minus_at", f32), ("sqrt_at", f32), ("dir_coef", f32), ("sqrt_a_prev", f32),
+                ("sigma", f32), ("temperature", f32), ("guidance", f32), ("v_param", i32), ("v_sqrt_a", f32),
+                ("v_sqrt_1ma", f32)]
+
+
+OUT_NHWC_F16, OUT_NCHW_F32, OUT_GEGLU_F16, OUT_ROWS_F32 = 0, 1, 2, 3
+
+EXPORTS = ["sdk_conv2d_plan", "sdk_conv2d", "sdk_group_norm_workspace", "sdk_group_norm_affine", "sdk_layer_norm",
+           "sdk_attention", "sdk_ddim_step", "sdk_ddpm_step", "sdk_timestep_embedding", "sdk_nchw_to_nhwc",
+           "sdk_last_error", "sdk_version", "sdk_kernel_name"]
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"sd_amd: HIP library not built ({LIB_PATH} missing); run __graft_entry__.build()")
+    L = C.CDLL(LIB_PATH)
+    L.sdk_conv2d_plan.argtypes = [C.POINTER(ConvArgs), C.POINTER(ConvPlanInfo)]
+    L.sdk_conv2d.argtypes = [C.POINTER(ConvArgs), vp]
+    L.sdk_group_norm_workspace.argtypes = [i32, i32, i32]
+    L.sdk_group_norm_workspace.restype = i64
+    L.sdk_group_norm_affine.argtypes = [C.POINTER(GroupNormArgs), vp]
+    L.sdk_layer_norm.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp, f32, vp]
+    L.sdk_attention.argtypes = [C.POINTER(AttentionArgs), vp]
+    L.sdk_ddim_step.argtypes = [C.POINTER(DdimArgs), vp]
+    L.sdk_ddpm_step.argtypes = [vp, vp, vp, vp, i64, f32, f32, f32, vp]
+    L.sdk_timestep_embedding.argtypes = [vp, vp, vp, i32, i32, vp]
+    L.sdk_nchw_to_nhwc.argtypes = [vp, vp, i32, i32, i32, i32, f32, vp]
+    L.sdk_last_error.restype = C.c_char_p
+    L.sdk_kernel_name.restype = C.c_char_p
+    L.sdk_kernel_name.argtypes = [i32]
+    for name in EXPORTS:
+        if not hasattr(L, name):
+            raise RuntimeError(f"sd_amd: {LIB_PATH} does not export {name}")
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().sdk_last_error().decode(errors="replace")
+        raise RuntimeError(f"sd_amd.{what} failed ({rc}): {msg}")

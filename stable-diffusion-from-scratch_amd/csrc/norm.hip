@@ -1,0 +1,242 @@
+// GroupNorm statistics and LayerNorm for gfx950 (HBM-bound, NHWC fp16 in).
+//
+// GroupNorm is split: this file produces per-(batch, channel) scale/shift
+// (gamma*rstd, beta - mean*gamma*rstd) and the conv kernel applies them (plus
+// SiLU) while staging its A tile, so the normalised tensor never round-trips
+// through HBM.  Statistics: pass 1 streams the tensor once with 16-B loads,
+// one thread per 8 channels, accumulating pivot-shifted sums (pivot = the
+// channel's value at pixel 0 of the image, so E[x^2]-E[x]^2 does not cancel
+// for offset activations); pass 2 merges chunks in double per channel and
+// channels into groups with Chan's parallel-variance formula.
+#include <algorithm>
+
+#include "common.h"
+
+namespace sdk {
+namespace {
+
+constexpr int GN_ROWS_PER_THREAD = 32;
+
+struct GnGeom {
+  int c8, nv, ry, chunk_rows, nchunks;
+};
+
+GnGeom gn_geom(int hw, int channels) {
+  GnGeom g;
+  g.c8 = channels / 8;
+  g.nv = (g.c8 + 255) / 256;
+  g.ry = g.nv > 1 ? 1 : std::max(1, 256 / g.c8);
+  g.chunk_rows = g.ry * GN_ROWS_PER_THREAD;
+  g.nchunks = (hw + g.chunk_rows - 1) / g.chunk_rows;
+  return g;
+}
+
+__device__ __forceinline__ h8 load_px(const half_t* s0, const half_t* s1, int c_split, int ld0, int ld1,
+                                      size_t pix, int c) {
+  if (c < c_split) return *reinterpret_cast<const h8*>(s0 + pix * ld0 + c);
+  return *reinterpret_cast<const h8*>(s1 + pix * ld1 + (c - c_split));
+}
+
+// grid (nchunks, batch); writes partial[b][chunk][c] = (S1, S2) of (x - pivot_c)
+__global__ void __launch_bounds__(256) gn_partial_kernel(const half_t* s0, const half_t* s1, int c_split, int ld0,
+                                                         int ld1, int hw, int channels, GnGeom g, float2* partial) {
+  extern __shared__ __attribute__((aligned(16))) float red[];   // [ry][c8*8] x 2
+  const int tid = threadIdx.x, chunk = blockIdx.x, b = blockIdx.y;
+  const int r0 = chunk * g.chunk_rows, r1 = min(hw, r0 + g.chunk_rows);
+  const size_t img = (size_t)b * hw;
+  const int ysub = tid / g.c8;
+  for (int vi = 0; vi < g.nv; ++vi) {
+    const int vec = g.nv > 1 ? tid + vi * 256 : tid % g.c8;
+    const bool active = vec < g.c8 && ysub < g.ry;
+    float sum[8], sq[8], piv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { sum[j] = 0.f; sq[j] = 0.f; piv[j] = 0.f; }
+    if (active) {
+      const int c = vec * 8;
+      h8 pv = load_px(s0, s1, c_split, ld0, ld1, img, c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) piv[j] = (float)pv[j];
+      const int rstart = r0 + (g.nv > 1 ? 0 : ysub);
+      const int rstep = g.nv > 1 ? 1 : g.ry;
+      for (int r = rstart; r < r1; r += rstep) {
+        h8 v = load_px(s0, s1, c_split, ld0, ld1, img + r, c);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = (float)v[j] - piv[j];
+          sum[j] += d;
+          sq[j] += d * d;
+        }
+      }
+    }
+    if (g.ry == 1) {
+      if (active) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          partial[((size_t)b * g.nchunks + chunk) * channels + vec * 8 + j] = make_float2(sum[j], sq[j]);
+      }
+      continue;
+    }
+    // reduce over ysub through LDS
+    const int C = g.c8 * 8;
+    if (active) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[ysub * C + vec * 8 + j] = sum[j];
+        red[(g.ry + ysub) * C + vec * 8 + j] = sq[j];
+      }
+    }
+    __syncthreads();
+    for (int c = tid; c < C; c += 256) {
+      float a = 0.f, q = 0.f;
+      for (int y = 0; y < g.ry; ++y) { a += red[y * C + c]; q += red[(g.ry + y) * C + c]; }
+      partial[((size_t)b * g.nchunks + chunk) * channels + c] = make_float2(a, q);
+    }
+  }
+}
+
+// grid (groups, batch), 64 threads (one wave): per channel merge chunks in double,
+// then Chan-merge the group's channels.
+__global__ void __launch_bounds__(64) gn_finalize_kernel(const half_t* s0, const half_t* s1, int c_split, int ld0,
+                                                         int ld1, int hw, int channels, int groups, GnGeom g,
+                                                         const float2* partial, float eps, const float* gamma,
+                                                         const float* beta, float* scale, float* shift) {
+  const int grp = blockIdx.x, b = blockIdx.y, lane = threadIdx.x;
+  const int cg = channels / groups, c0 = grp * cg;
+  const size_t img = (size_t)b * hw;
+  // each lane owns channels c0+lane, c0+lane+64, ... (cg <= 64*4)
+  double mean_sum = 0.0, m2_sum = 0.0, msq_sum = 0.0;
+  const double n = (double)hw;
+  for (int ci = lane; ci < cg; ci += 64) {
+    const int c = c0 + ci;
+    double a1 = 0.0, a2 = 0.0;
+    for (int k = 0; k < g.nchunks; ++k) {
+      const float2 v = partial[((size_t)b * g.nchunks + k) * channels + c];
+      a1 += v.x;
+      a2 += v.y;
+    }
+    // the pivot pass 1 subtracted: this channel's value at pixel 0 of the image
+    const float piv = c < c_split ? (float)s0[img * ld0 + c] : (float)s1[img * ld1 + (c - c_split)];
+    const double mc = (double)piv + a1 / n;
+    const double m2c = a2 - a1 * a1 / n;
+    mean_sum += mc;
+    msq_sum += mc * mc;
+    m2_sum += m2c;
+  }
+  // wave reduce
+  for (int off = 32; off > 0; off >>= 1) {
+    mean_sum += __shfl_xor(mean_sum, off, 64);
+    msq_sum += __shfl_xor(msq_sum, off, 64);
+    m2_sum += __shfl_xor(m2_sum, off, 64);
+  }
+  const double mg = mean_sum / cg;
+  // sum over channels of n*(mc - mg)^2 = n*(sum mc^2 - cg*mg^2)
+  double m2g = m2_sum + n * (msq_sum - cg * mg * mg);
+  if (m2g < 0) m2g = 0;
+  const double var = m2g / (n * cg);
+  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float meanf = (float)mg;
+  for (int ci = lane; ci < cg; ci += 64) {
+    const int c = c0 + ci;
+    const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+    const float sc = gm * rstd;
+    scale[(size_t)b * channels + c] = sc;
+    shift[(size_t)b * channels + c] = bt - meanf * sc;
+  }
+}
+
+// LayerNorm: one wave per row, row cached in registers (cols <= 64*8*MAXV).
+constexpr int LN_MAXV = 4;
+__global__ void __launch_bounds__(256) layer_norm_kernel(const half_t* x, half_t* y, int rows, int cols, int ldx,
+                                                         int ldy, const float* gamma, const float* beta, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int c8 = cols / 8;
+  const half_t* xr = x + (size_t)row * ldx;
+  h8 v[LN_MAXV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int k = lane + 64 * i;
+    v[i] = h8{};
+    if (k < c8) {
+      v[i] = *reinterpret_cast<const h8*>(xr + k * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += (float)v[i][j];
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  const float mean = s / cols;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int k = lane + 64 * i;
+    if (k < c8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = (float)v[i][j] - mean;
+        q += d * d;
+      }
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) q += __shfl_xor(q, off, 64);
+  const float rstd = rsqrtf(q / cols + eps);
+  half_t* yr = y + (size_t)row * ldy;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int k = lane + 64 * i;
+    if (k < c8) {
+      h8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = k * 8 + j;
+        o[j] = (half_t)(((float)v[i][j] - mean) * rstd * gamma[c] + beta[c]);
+      }
+      *reinterpret_cast<h8*>(yr + k * 8) = o;
+    }
+  }
+}
+
+}  // namespace
+}  // namespace sdk
+
+using namespace sdk;
+
+extern "C" int64_t sdk_group_norm_workspace(int32_t batch, int32_t hw, int32_t channels) {
+  if (batch <= 0 || hw <= 0 || channels <= 0) return 0;
+  GnGeom g = gn_geom(hw, channels);
+  return (int64_t)batch * g.nchunks * channels * (int64_t)sizeof(float2);
+}
+
+extern "C" int sdk_group_norm_affine(const sdk_group_norm_args* a, sdk_stream_t stream) {
+  if (!a || !a->src0 || !a->scale || !a->shift) return fail(SDK_EINVAL, "group_norm: null pointer");
+  if (a->channels % 8 || a->channels % a->groups || a->c_split % 8 || a->c_split <= 0 || a->c_split > a->channels)
+    return fail(SDK_EINVAL, "group_norm: channels/c_split must be multiples of 8, channels % groups == 0");
+  if (a->channels / a->groups > 256) return fail(SDK_EINVAL, "group_norm: > 256 channels per group");
+  if (a->c_split < a->channels && !a->src1) return fail(SDK_EINVAL, "group_norm: concat without src1");
+  if (a->ld0 % 8 || (a->c_split < a->channels && a->ld1 % 8)) return fail(SDK_EINVAL, "group_norm: ld % 8");
+  if (a->channels / 8 > 512) return fail(SDK_EINVAL, "group_norm: channels > 4096");
+  const int64_t need = sdk_group_norm_workspace(a->batch, a->hw, a->channels);
+  if (!a->workspace || a->workspace_bytes < need) return fail(SDK_EWORKSPACE, "group_norm: workspace too small");
+  GnGeom g = gn_geom(a->hw, a->channels);
+  hipStream_t s = (hipStream_t)stream;
+  const size_t lds = g.ry > 1 ? (size_t)2 * g.ry * g.c8 * 8 * sizeof(float) : 0;
+  hipLaunchKernelGGL(gn_partial_kernel, dim3(g.nchunks, a->batch), dim3(256), lds, s, (const half_t*)a->src0,
+                     (const half_t*)a->src1, a->c_split, a->ld0, a->ld1, a->hw, a->channels, g,
+                     (float2*)a->workspace);
+  if (int e = check_launch("gn_partial")) return e;
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3(a->groups, a->batch), dim3(64), 0, s, (const half_t*)a->src0,
+                     (const half_t*)a->src1, a->c_split, a->ld0, a->ld1, a->hw, a->channels, a->groups, g,
+                     (const float2*)a->workspace, a->eps, a->gamma, a->beta, a->scale, a->shift);
+  return check_launch("gn_finalize");
+}
+
+extern "C" int sdk_layer_norm(const void* x, void* y, int32_t rows, int32_t cols, int32_t ld_x, int32_t ld_y,
+                              const float* gamma, const float* beta, float eps, sdk_stream_t stream) {
+  if (!x || !y || !gamma || !beta) return fail(SDK_EINVAL, "layer_norm: null pointer");
+  if (cols % 8 || ld_x % 8 || ld_y % 8 || cols > 64 * 8 * LN_MAXV) return fail(SDK_EINVAL, "layer_norm: cols");
+  if (rows <= 0) return SDK_OK;
+  hipLaunchKernelGGL(layer_norm_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream,
+                     (const half_t*)x, (half_t*)y, rows, cols, ld_x, ld_y, gamma, beta, eps);
+  return check_launch("layer_norm");
+}

@@ -1,0 +1,169 @@
+// Sampler-side elementwise kernels (HBM-bound, fp32) and layout glue, plus the
+// library's error/introspection entry points.
+//
+// The DDIM / DDPM updates are compiled with floating-point contraction OFF
+// (see the pragma) so each a*b+c is two correctly-rounded operations, exactly
+// as torch's CPU kernels evaluate the reference expression; fed the same
+// inputs the result is bit-identical to the oracle.
+#include <cmath>
+#include <cstdio>
+
+#include "common.h"
+
+#pragma clang fp contract(off)
+
+namespace sdk {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(SDK_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+  return SDK_OK;
+}
+
+namespace {
+
+__global__ void __launch_bounds__(256) ddim_step_kernel(sdk_ddim_args a) {
+  const int64_t n4 = a.n / 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    f4 x = reinterpret_cast<const f4*>(a.x)[i];
+    f4 e = reinterpret_cast<const f4*>(a.e)[i];
+    if (a.e_uncond) {
+      const f4 u = reinterpret_cast<const f4*>(a.e_uncond)[i];
+      f4 d;
+      for (int j = 0; j < 4; ++j) d[j] = e[j] - u[j];
+      for (int j = 0; j < 4; ++j) e[j] = u[j] + a.guidance * d[j];
+    }
+    if (a.v_param) {
+      for (int j = 0; j < 4; ++j) {
+        const float t0 = a.v_sqrt_a * e[j];
+        const float t1 = a.v_sqrt_1ma * x[j];
+        e[j] = t0 + t1;
+      }
+    }
+    f4 nz = {0.f, 0.f, 0.f, 0.f};
+    if (a.noise) nz = reinterpret_cast<const f4*>(a.noise)[i];
+    f4 xp, p0;
+    for (int j = 0; j < 4; ++j) {
+      const float t1 = a.sqrt_one_minus_at * e[j];
+      const float t2 = x[j] - t1;
+      const float pred = t2 / a.sqrt_at;
+      const float dir = a.dir_coef * e[j];
+      const float t3 = a.sqrt_a_prev * pred;
+      const float t4 = t3 + dir;
+      const float nn = (a.sigma * nz[j]) * a.temperature;
+      xp[j] = t4 + nn;
+      p0[j] = pred;
+    }
+    reinterpret_cast<f4*>(a.x_prev)[i] = xp;
+    if (a.pred_x0) reinterpret_cast<f4*>(a.pred_x0)[i] = p0;
+  }
+}
+
+__global__ void __launch_bounds__(256) ddpm_step_kernel(const float* x, const float* eps, const float* noise,
+                                                        float* out, int64_t n, float inv_sqrt_alpha, float coef,
+                                                        float sigma) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float t = coef * eps[i];
+    float v = inv_sqrt_alpha * (x[i] - t);
+    if (noise) v = v + sigma * noise[i];
+    out[i] = v;
+  }
+}
+
+__global__ void temb_kernel(const int64_t* t, const float* freqs, half_t* out, int batch, int dim) {
+  const int half = dim / 2;
+  const int b = blockIdx.x;
+  const float tf = (float)t[b];
+  for (int k = threadIdx.x; k < dim; k += blockDim.x) {
+    float v = 0.f;
+    if (k < half) v = cosf(tf * freqs[k]);
+    else if (k < 2 * half) v = sinf(tf * freqs[k - half]);
+    out[(size_t)b * dim + k] = (half_t)v;
+  }
+}
+
+__global__ void __launch_bounds__(256) nchw_to_nhwc_kernel(const float* x, half_t* y, int C, int HW, int Cp,
+                                                           float scale) {
+  // grid (ceil(HW/64), B); tile 64 pixels x C through LDS so both sides are coalesced
+  __shared__ float tile[64][33];
+  const int b = blockIdx.y, p0 = blockIdx.x * 64;
+  for (int c0 = 0; c0 < Cp; c0 += 32) {
+    for (int e = threadIdx.x; e < 32 * 64; e += 256) {
+      const int cc = e / 64, pp = e % 64;
+      const int c = c0 + cc, pix = p0 + pp;
+      float v = 0.f;
+      if (c < C && pix < HW) v = x[((size_t)b * C + c) * HW + pix] * scale;
+      tile[pp][cc] = v;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 32 * 64; e += 256) {
+      const int pp = e / 32, cc = e % 32;
+      const int c = c0 + cc, pix = p0 + pp;
+      if (c < Cp && pix < HW) y[((size_t)b * HW + pix) * Cp + c] = (half_t)tile[pp][cc];
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace
+}  // namespace sdk
+
+using namespace sdk;
+
+extern "C" int sdk_ddim_step(const sdk_ddim_args* a, sdk_stream_t stream) {
+  if (!a || !a->x || !a->e || !a->x_prev) return fail(SDK_EINVAL, "ddim_step: null pointer");
+  if (a->n <= 0 || a->n % 4) return fail(SDK_EINVAL, "ddim_step: n must be a positive multiple of 4");
+  const int64_t n4 = a->n / 4;
+  const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
+  hipLaunchKernelGGL(ddim_step_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, *a);
+  return check_launch("ddim_step");
+}
+
+extern "C" int sdk_ddpm_step(const float* x, const float* eps, const float* noise, float* out, int64_t n,
+                             float inv_sqrt_alpha, float coef, float sigma, sdk_stream_t stream) {
+  if (!x || !eps || !out || n <= 0) return fail(SDK_EINVAL, "ddpm_step: bad args");
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 2048);
+  hipLaunchKernelGGL(ddpm_step_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, eps, noise, out, n,
+                     inv_sqrt_alpha, coef, sigma);
+  return check_launch("ddpm_step");
+}
+
+extern "C" int sdk_timestep_embedding(const int64_t* t, const float* freqs, void* out, int32_t batch, int32_t dim,
+                                      sdk_stream_t stream) {
+  if (!t || !freqs || !out || batch <= 0 || dim <= 0) return fail(SDK_EINVAL, "timestep_embedding: bad args");
+  hipLaunchKernelGGL(temb_kernel, dim3(batch), dim3(256), 0, (hipStream_t)stream, t, freqs, (half_t*)out, batch,
+                     dim);
+  return check_launch("timestep_embedding");
+}
+
+extern "C" int sdk_nchw_to_nhwc(const float* x, void* y, int32_t batch, int32_t channels, int32_t hw, int32_t c_pad,
+                                float scale, sdk_stream_t stream) {
+  if (!x || !y || batch <= 0 || channels <= 0 || hw <= 0 || c_pad < channels)
+    return fail(SDK_EINVAL, "nchw_to_nhwc: bad args");
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3((hw + 63) / 64, batch), dim3(256), 0, (hipStream_t)stream, x,
+                     (half_t*)y, channels, hw, c_pad, scale);
+  return check_launch("nchw_to_nhwc");
+}
+
+extern "C" const char* sdk_last_error(void) { return g_last_error.c_str(); }
+
+extern "C" int sdk_version(void) { return 1; }
+
+extern "C" const char* sdk_kernel_name(int32_t variant) {
+  switch (variant) {
+    case 0: return "conv_igemm_kernel";
+    case 1: return "conv_igemm_kernel+splitk_reduce_kernel";
+    default: return "unknown";
+  }
+}

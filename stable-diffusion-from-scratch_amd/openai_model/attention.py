@@ -1,0 +1,240 @@
+"""Mirror of ``openai_model/attention.py`` — SpatialTransformer / BasicTransformerBlock /
+CrossAttention / GEGLU FeedForward / AttentionBlock (+ QKVAttentionLegacy), HIP-backed.
+
+Parameter names and constructor signatures follow the reference so SD
+checkpoints and ``Diffusion/config.yaml`` params load unchanged.  Execution
+(``_run``) works on NHWC fp16 token matrices:
+
+* q/k/v projections are one fused GEMM for self-attention (concatenated
+  weights), the context K/V of cross-attention is one GEMM computed once per
+  conditioning tensor (step-invariant across the sampler loop);
+* the softmax(QK^T)V core is ``sdk_attention`` (flash-style, fp32 softmax);
+* to_out / FF-out / proj_out GEMMs fuse the residual add in their epilogue, the
+  GEGLU projection fuses ``x * gelu(gate)`` in its epilogue;
+* the SpatialTransformer GroupNorm is applied inside the proj_in GEMM prologue.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+from torch import nn
+
+from .. import ops
+from .utils import conv_nd, normalization, zero_module
+
+
+def Normalize(in_channels):
+    return torch.nn.GroupNorm(num_groups=32, num_channels=in_channels, eps=1e-6, affine=True)
+
+
+def _gn_prep(gn: nn.GroupNorm, dev):
+    gn._g = gn.weight.detach().to(dev, torch.float32).contiguous()
+    gn._b = gn.bias.detach().to(dev, torch.float32).contiguous()
+
+
+def _gn_stats(gn: nn.GroupNorm, x):
+    return ops.group_norm_affine(x, gn._g, gn._b, gn.eps, gn.num_groups)
+
+
+def _ln_prep(ln: nn.LayerNorm, dev):
+    ln._g = ln.weight.detach().to(dev, torch.float32).contiguous()
+    ln._b = ln.bias.detach().to(dev, torch.float32).contiguous()
+
+
+class CrossAttention(nn.Module):
+    """Reference ``attention.py:24-117``: no-bias q/k/v, to_out Linear+Dropout, scale d^-1/2."""
+
+    def __init__(self, query_dim, context_dim=None, heads=8, dim_head=64, dropout=0.):
+        super().__init__()
+        inner_dim = dim_head * heads
+        self.self_attn = context_dim is None
+        context_dim = query_dim if context_dim is None else context_dim
+        self.scale = dim_head ** -0.5
+        self.heads = heads
+        self.dim_head = dim_head
+        self.to_q = nn.Linear(query_dim, inner_dim, bias=False)
+        self.to_k = nn.Linear(context_dim, inner_dim, bias=False)
+        self.to_v = nn.Linear(context_dim, inner_dim, bias=False)
+        self.to_out = nn.Sequential(nn.Linear(inner_dim, query_dim), nn.Dropout(dropout))
+
+    def _prepare(self, dev):
+        qd = self.to_q.in_features
+        cd = self.to_k.in_features
+        if self.self_attn:
+            w = torch.cat([self.to_q.weight, self.to_k.weight, self.to_v.weight], 0)
+            self._pc_qkv = ops.PackedConv([(w, qd)], None, device=dev)
+        self._pc_q = ops.PackedConv([(self.to_q.weight, qd)], None, device=dev)
+        self._pc_kv = ops.PackedConv([(torch.cat([self.to_k.weight, self.to_v.weight], 0), cd)], None, device=dev)
+        self._pc_o = ops.PackedConv([(self.to_out[0].weight, self.heads * self.dim_head)], self.to_out[0].bias,
+                                    device=dev)
+
+    def context_kv(self, ctx2d):
+        """K|V of the conditioning, [B*L, 2*inner] — computed once per conditioning tensor."""
+        return ops.linear(self._pc_kv, ctx2d)
+
+    def _run(self, t, residual, B, N, kv=None, Lc=None):
+        inner = self.heads * self.dim_head
+        if kv is None:
+            if self.self_attn:
+                qkv = ops.linear(self._pc_qkv, t)
+                q, k, v, nk = qkv[:, :inner], qkv[:, inner:2 * inner], qkv[:, 2 * inner:], N
+            else:   # context defaults to x (reference: default(context, x)) — only legal if dims match
+                q = ops.linear(self._pc_q, t)
+                kvx = ops.linear(self._pc_kv, t)
+                k, v, nk = kvx[:, :inner], kvx[:, inner:], N
+        else:
+            q = ops.linear(self._pc_q, t)
+            k, v, nk = kv[:, :inner], kv[:, inner:], Lc
+        o = ops.attention(q, k, v, batch=B, heads=self.heads, nq=N, nk=nk, head_dim=self.dim_head, scale=self.scale)
+        return ops.linear(self._pc_o, o, residual=residual)
+
+
+class GELU(nn.Module):
+    """GEGLU projection (reference ``attention.py:129-141``): Linear(dim_in, 2*dim_out); x*gelu(gate)."""
+
+    def __init__(self, dim_in, dim_out):
+        super().__init__()
+        self.proj = nn.Linear(dim_in, dim_out * 2)
+
+
+class FeedForward(nn.Module):
+    """Reference ``attention.py:146-172`` (glu=True path: GELU → Dropout → Linear)."""
+
+    def __init__(self, dim, dim_out=None, mult=4, glu=False, dropout=0.):
+        super().__init__()
+        inner_dim = int(dim * mult)
+        dim_out = dim if dim_out is None else dim_out
+        if not glu:
+            raise NotImplementedError("sd_amd: only the gated (GEGLU) feed-forward is on the SD path")
+        self.net = nn.Sequential(GELU(dim, inner_dim), nn.Dropout(dropout), nn.Linear(inner_dim, dim_out))
+
+    def _prepare(self, dev):
+        p = self.net[0].proj
+        self._pc1 = ops.PackedConv([(p.weight, p.in_features)], p.bias, geglu=True, device=dev)
+        self._pc2 = ops.PackedConv([(self.net[2].weight, self.net[2].in_features)], self.net[2].bias, device=dev)
+
+    def _run(self, t, residual):
+        g = ops.linear(self._pc1, t, out_mode=ops.OUT_GEGLU_F16)
+        return ops.linear(self._pc2, g, residual=residual)
+
+
+class BasicTransformerBlock(nn.Module):
+    """Reference ``attention.py:187-257``: x += attn1(LN x); x += attn2(LN x, ctx); x += FF(LN x)."""
+
+    def __init__(self, dim, n_heads, d_head, dropout=0., context_dim=None, gated_ff=True, checkpoint=True):
+        super().__init__()
+        self.attn1 = CrossAttention(query_dim=dim, heads=n_heads, dim_head=d_head, dropout=dropout)
+        self.ff = FeedForward(dim=dim, dropout=dropout, glu=gated_ff)
+        self.attn2 = CrossAttention(query_dim=dim, context_dim=context_dim, heads=n_heads, dim_head=d_head,
+                                    dropout=dropout)
+        self.norm1 = nn.LayerNorm(dim)
+        self.norm2 = nn.LayerNorm(dim)
+        self.norm3 = nn.LayerNorm(dim)
+        self.checkpoint = checkpoint
+
+    def _prepare(self, dev):
+        for m in (self.attn1, self.attn2, self.ff):
+            m._prepare(dev)
+        for n in (self.norm1, self.norm2, self.norm3):
+            _ln_prep(n, dev)
+
+    def _run(self, tok, B, N, kv=None, Lc=None):
+        t = ops.layer_norm(tok, self.norm1._g, self.norm1._b, self.norm1.eps)
+        tok = self.attn1._run(t, tok, B, N)
+        t = ops.layer_norm(tok, self.norm2._g, self.norm2._b, self.norm2.eps)
+        tok = self.attn2._run(t, tok, B, N, kv, Lc)
+        t = ops.layer_norm(tok, self.norm3._g, self.norm3._b, self.norm3.eps)
+        return self.ff._run(t, tok)
+
+
+class SpatialTransformer(nn.Module):
+    """Reference ``attention.py:303-363``: GN(eps 1e-6) → proj_in 1x1 → blocks → proj_out 1x1 → + x."""
+
+    def __init__(self, in_channels, n_heads, d_head, depth=1, dropout=0., context_dim=None):
+        super().__init__()
+        self.in_channels = in_channels
+        inner_dim = n_heads * d_head
+        self.inner_dim = inner_dim
+        self.norm = Normalize(in_channels)
+        self.proj_in = nn.Conv2d(in_channels, inner_dim, kernel_size=1, stride=1, padding=0)
+        self.transformer_blocks = nn.ModuleList(
+            [BasicTransformerBlock(inner_dim, n_heads, d_head, dropout=dropout, context_dim=context_dim)
+             for _ in range(depth)])
+        self.proj_out = zero_module(nn.Conv2d(inner_dim, in_channels, kernel_size=1, stride=1, padding=0))
+
+    def _prepare(self, dev):
+        _gn_prep(self.norm, dev)
+        self._pc_in = ops.PackedConv([(self.proj_in.weight, self.in_channels)], self.proj_in.bias, device=dev)
+        self._pc_out = ops.PackedConv([(self.proj_out.weight, self.inner_dim)], self.proj_out.bias, device=dev)
+        for blk in self.transformer_blocks:
+            blk._prepare(dev)
+
+    def context_kv(self, ctx2d):
+        return [blk.attn2.context_kv(ctx2d) for blk in self.transformer_blocks]
+
+    def _run(self, x, kvs=None, Lc=None):
+        B, H, W, Cc = x.shape
+        gn = _gn_stats(self.norm, x)
+        h = ops.conv2d(self._pc_in, x, gn=gn, silu=False)
+        tok = h.view(B * H * W, self.inner_dim)
+        for i, blk in enumerate(self.transformer_blocks):
+            tok = blk._run(tok, B, H * W, None if kvs is None else kvs[i], Lc)
+        return ops.conv2d(self._pc_out, tok.view(B, H, W, self.inner_dim), residual=x)
+
+
+class QKVAttentionLegacy(nn.Module):
+    """Reference ``attention.py:490-526``: qkv viewed [T, 3, H, ch]; softmax scale 1/sqrt(sqrt(ch))
+    (SURVEY quirk Q3 — reproduced for parity)."""
+
+    def __init__(self, n_heads):
+        super().__init__()
+        self.n_heads = n_heads
+
+    def scale(self, ch):
+        return 1.0 / math.sqrt(math.sqrt(ch))
+
+
+class FlashAttention(nn.Module):
+    """Reference ``attention.py:369-404`` (use_new_attention_order): same [T, 3, H, d] view, scale d^-1/2."""
+
+    def __init__(self, n_heads):
+        super().__init__()
+        self.n_heads = n_heads
+
+    def scale(self, ch):
+        return 1.0 / math.sqrt(ch)
+
+
+class AttentionBlock(nn.Module):
+    """Reference ``attention.py:539-597``: GN32 → Conv1d qkv → attention → Conv1d proj_out → + x."""
+
+    def __init__(self, channels, num_heads=1, num_head_channels=-1, use_checkpoint=False,
+                 use_new_attention_order=False):
+        super().__init__()
+        self.channels = channels
+        if num_head_channels == -1:
+            self.num_heads = num_heads
+        else:
+            assert channels % num_head_channels == 0
+            self.num_heads = channels // num_head_channels
+        self.use_checkpoint = use_checkpoint
+        self.norm = normalization(channels)
+        self.qkv = conv_nd(1, channels, channels * 3, 1)
+        self.attention = FlashAttention(self.num_heads) if use_new_attention_order else \
+            QKVAttentionLegacy(self.num_heads)
+        self.proj_out = zero_module(conv_nd(1, channels, channels, 1))
+
+    def _prepare(self, dev):
+        self.norm._prepare(dev)
+        self._pc_qkv = ops.PackedConv([(self.qkv.weight, self.channels)], self.qkv.bias, device=dev)
+        self._pc_proj = ops.PackedConv([(self.proj_out.weight, self.channels)], self.proj_out.bias, device=dev)
+
+    def _run(self, x):
+        B, H, W, Cc = x.shape
+        gn = self.norm.stats(x)
+        qkv = ops.conv2d(self._pc_qkv, x, gn=gn).view(B * H * W, 3 * Cc)
+        ch = Cc // self.num_heads
+        o = ops.attention(qkv[:, :Cc], qkv[:, Cc:2 * Cc], qkv[:, 2 * Cc:], batch=B, heads=self.num_heads,
+                          nq=H * W, nk=H * W, head_dim=ch, scale=self.attention.scale(ch))
+        return ops.conv2d(self._pc_proj, o.view(B, H, W, Cc), residual=x)

@@ -1,0 +1,393 @@
+"""Tensor-level wrappers over the C ABI (libsdk_amd.so).
+
+Activations are NHWC fp16 CUDA tensors ``[B, H, W, C]`` (tokens ``[B, N, C]`` are
+the ``W = 1`` case).  A conv source may be a 2-tuple ``(a, b)`` meaning the
+channel concat ``cat([a, b], -1)``, read zero-copy by the kernels.
+
+There is no CPU or eager-PyTorch fallback: a non-CUDA tensor raises TypeError,
+a library failure raises RuntimeError.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+
+import torch
+
+from . import _lib
+from ._lib import (AttentionArgs, ConvArgs, ConvPlanInfo, DdimArgs, GroupNormArgs, OUT_GEGLU_F16, OUT_NCHW_F32,
+                   OUT_NHWC_F16, OUT_ROWS_F32, check, lib)
+
+BK = 64          # K tile of the conv kernel (packed weight column padding)
+BN = 128         # N tile (packed weight row padding)
+
+
+def _stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _need_cuda(t: torch.Tensor, what: str, dtype=torch.float16):
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise TypeError(f"sd_amd.{what}: expected a CUDA tensor (HIP path only, no CPU fallback)")
+    if dtype is not None and t.dtype != dtype:
+        raise TypeError(f"sd_amd.{what}: expected {dtype}, got {t.dtype}")
+
+
+# --------------------------------------------------------------------------- workspace
+
+class _Workspace:
+    """One growable per-device scratch buffer (split-K slabs, GroupNorm partials).
+    Calls are stream-ordered on one stream, so a single buffer is safe to reuse."""
+
+    def __init__(self):
+        self.buf = {}
+
+    def get(self, nbytes: int, device) -> torch.Tensor:
+        key = torch.device(device).index
+        b = self.buf.get(key)
+        if b is None or b.numel() < nbytes:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("sd_amd: workspace must be sized before graph capture (run one warm-up step)")
+            b = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+            self.buf[key] = b
+        return b
+
+
+WORKSPACE = _Workspace()
+
+
+# --------------------------------------------------------------------------- sources
+
+def _as_pair(x):
+    if isinstance(x, tuple):
+        a, b = x
+        return a, b
+    return x, None
+
+
+def src_shape(x):
+    a, b = _as_pair(x)
+    B, H, W, C0 = a.shape
+    return B, H, W, C0 + (b.shape[-1] if b is not None else 0)
+
+
+def _fill_src(s: "_lib.ConvSrc", x, ksize, stride, pad, upsample, gn, silu):
+    a, b = _as_pair(x)
+    _need_cuda(a, "conv2d")
+    if a.stride(-1) != 1:
+        raise ValueError("sd_amd.conv2d: source channels must be contiguous")
+    B, H, W, C0 = a.shape
+    s.src0 = a.data_ptr()
+    s.ld0 = a.stride(2) if a.dim() == 4 else a.stride(1)
+    if b is not None:
+        _need_cuda(b, "conv2d")
+        s.src1 = b.data_ptr()
+        s.ld1 = b.stride(2)
+        s.c_split = C0
+        s.cin = C0 + b.shape[-1]
+    else:
+        s.src1 = None
+        s.ld1 = 0
+        s.c_split = C0
+        s.cin = C0
+    s.h, s.w = H, W
+    s.ksize, s.stride, s.pad, s.upsample = ksize, stride, pad, 1 if upsample else 0
+    if gn is not None:
+        s.gn_scale, s.gn_shift = gn[0].data_ptr(), gn[1].data_ptr()
+    else:
+        s.gn_scale = s.gn_shift = None
+    s.silu = 1 if silu else 0
+    return B, H, W
+
+
+# --------------------------------------------------------------------------- packed weights
+
+class PackedConv:
+    """A conv / linear weight packed for the implicit-GEMM kernel.
+
+    ``segments``: list of (weight [N, Cin, k, k] or [N, Cin], cin_src) — cin_src is
+    the channel count of the NHWC source feeding that segment (>= Cin; extra
+    channels get zero weights).  Packed layout: fp16 [roundup(N,128)][sum_s k*k*roundup(cin_src,64)],
+    tap-major then channel.  ``geglu`` interleaves the (x, gate) halves of a
+    GEGLU projection in 32-row groups so one wave holds both.
+    """
+
+    def __init__(self, segments, bias=None, geglu=False, device="cuda"):
+        cols, self.seg_geom = [], []
+        n_out = None
+        for w, cin_src in segments:
+            w = w.detach().float()
+            if w.dim() == 2:
+                w = w[:, :, None, None]
+            if w.dim() == 3:                      # Conv1d [N, Cin, 1]
+                w = w[:, :, :, None]
+            N, Cin, kh, kw = w.shape
+            assert kh == kw, "square kernels only"
+            if n_out is None:
+                n_out = N
+            assert N == n_out
+            cin_pad = (cin_src + BK - 1) // BK * BK
+            wp = torch.zeros(N, kh, kw, cin_pad, dtype=torch.float32, device=w.device)
+            wp[:, :, :, :Cin] = w.permute(0, 2, 3, 1)
+            cols.append(wp.reshape(N, -1))
+            self.seg_geom.append((kh, cin_src))
+        Wt = torch.cat(cols, dim=1)
+        b = bias.detach().float().clone() if bias is not None else None
+        if geglu:
+            inner = n_out // 2
+            assert inner % 32 == 0
+            idx = []
+            for q in range(inner // 32):
+                idx += list(range(32 * q, 32 * q + 32)) + list(range(inner + 32 * q, inner + 32 * q + 32))
+            idx = torch.tensor(idx, device=Wt.device)
+            Wt = Wt[idx]
+            if b is not None:
+                b = b[idx.to(b.device)]
+        self.N = n_out
+        self.geglu = geglu
+        npad = (n_out + BN - 1) // BN * BN
+        Wfull = torch.zeros(npad, Wt.shape[1], dtype=torch.float32, device=Wt.device)
+        Wfull[:n_out] = Wt
+        self.weight = Wfull.to(device=device, dtype=torch.float16).contiguous()
+        self.k_total = self.weight.shape[1]
+        self.bias = b.to(device=device, dtype=torch.float32).contiguous() if b is not None else None
+
+
+def conv2d(pc: PackedConv, x, *, ksize=None, stride=1, pad=None, upsample=False, gn=None, silu=False,
+           seg2=None, bias=True, row_bias=None, residual=None, out_mode=OUT_NHWC_F16, out=None):
+    """Run the implicit-GEMM conv.  ``seg2`` = (x2, gn2, silu2) adds a fused 1x1 K segment.
+    ``row_bias`` = (fp32 tensor [B, ld], column offset) — the per-(batch, channel) add."""
+    a = ConvArgs()
+    k0 = pc.seg_geom[0][0] if ksize is None else ksize
+    if pad is None:
+        pad = k0 // 2
+    B, H, W = _fill_src(a.seg[0], x, k0, stride, pad, upsample, gn, silu)
+    lh, lw = (2 * H, 2 * W) if upsample else (H, W)
+    Ho = (lh + 2 * pad - k0) // stride + 1
+    Wo = (lw + 2 * pad - k0) // stride + 1
+    a.nseg = 1
+    if seg2 is not None:
+        x2, gn2, silu2 = seg2
+        _fill_src(a.seg[1], x2, 1, 1, 0, False, gn2, silu2)
+        a.nseg = 2
+    a.batch, a.ho, a.wo, a.cout = B, Ho, Wo, pc.N
+    a.weight = pc.weight.data_ptr()
+    a.k_total = pc.k_total
+    a.bias = pc.bias.data_ptr() if (bias and pc.bias is not None) else None
+    if row_bias is not None:
+        rb, off = row_bias
+        a.row_bias = rb.data_ptr() + 4 * off
+        a.row_bias_ld = rb.stride(0)
+    dev = (x[0] if isinstance(x, tuple) else x).device
+    if out is None:
+        if out_mode == OUT_NHWC_F16:
+            out = torch.empty(B, Ho, Wo, pc.N, dtype=torch.float16, device=dev)
+        elif out_mode == OUT_GEGLU_F16:
+            out = torch.empty(B, Ho, Wo, pc.N // 2, dtype=torch.float16, device=dev)
+        elif out_mode == OUT_NCHW_F32:
+            out = torch.empty(B, pc.N, Ho, Wo, dtype=torch.float32, device=dev)
+        else:
+            out = torch.empty(B, Ho, Wo, pc.N, dtype=torch.float32, device=dev)
+    a.out = out.data_ptr()
+    a.out_ld = out.shape[-1] if out_mode != OUT_NCHW_F32 else 0
+    a.out_mode = out_mode
+    if residual is not None:
+        _need_cuda(residual, "conv2d residual")
+        a.residual = residual.data_ptr()
+        a.res_ld = residual.shape[-1]
+    info = ConvPlanInfo()
+    check(lib().sdk_conv2d_plan(C.byref(a), C.byref(info)), "conv2d_plan")
+    if info.workspace_bytes > 0:
+        ws = WORKSPACE.get(info.workspace_bytes, dev)
+        a.workspace = ws.data_ptr()
+        a.workspace_bytes = ws.numel()
+    if PROFILER.active:
+        PROFILER.begin("conv", info)
+    check(lib().sdk_conv2d(C.byref(a), _stream()), "conv2d")
+    if PROFILER.active:
+        PROFILER.end()
+    return out
+
+
+def linear(pc: PackedConv, x2d, *, silu=False, residual=None, out_mode=OUT_NHWC_F16, out=None, bias=True):
+    """Token GEMM: x2d [M, K] fp16 → [M, N]; a 1x1 conv over an M x 1 image."""
+    M = x2d.shape[0]
+    x4 = x2d.view(1, M, 1, x2d.shape[-1]) if x2d.stride(-1) == 1 and x2d.is_contiguous() else None
+    if x4 is None:
+        x4 = x2d.as_strided((1, M, 1, x2d.shape[1]), (0, x2d.stride(0), x2d.stride(0), 1))
+    res4 = residual.view(1, M, 1, residual.shape[-1]) if residual is not None else None
+    y = conv2d(pc, x4, ksize=1, pad=0, silu=silu, residual=res4, out_mode=out_mode, bias=bias,
+               out=None if out is None else out.view(1, M, 1, out.shape[-1]))
+    return y.view(M, y.shape[-1])
+
+
+# --------------------------------------------------------------------------- normalisation
+
+def group_norm_affine(x, gamma, beta, eps, groups=32):
+    """Per-(batch, channel) (scale, shift) fp32 [B, C] of GroupNorm(x) for the conv prologue."""
+    a0, a1 = _as_pair(x)
+    _need_cuda(a0, "group_norm")
+    B, H, W, Ch = src_shape(x)
+    args = GroupNormArgs()
+    args.src0 = a0.data_ptr()
+    args.ld0 = a0.stride(2)
+    if a1 is not None:
+        args.src1 = a1.data_ptr()
+        args.ld1 = a1.stride(2)
+    args.c_split = a0.shape[-1]
+    args.batch, args.hw, args.channels, args.groups, args.eps = B, H * W, Ch, groups, eps
+    args.gamma = gamma.data_ptr()
+    args.beta = beta.data_ptr()
+    scale = torch.empty(B, Ch, dtype=torch.float32, device=a0.device)
+    shift = torch.empty(B, Ch, dtype=torch.float32, device=a0.device)
+    args.scale, args.shift = scale.data_ptr(), shift.data_ptr()
+    need = lib().sdk_group_norm_workspace(B, H * W, Ch)
+    ws = WORKSPACE.get(need, a0.device)
+    args.workspace, args.workspace_bytes = ws.data_ptr(), ws.numel()
+    if PROFILER.active:
+        PROFILER.begin("group_norm", None)
+    check(lib().sdk_group_norm_affine(C.byref(args), _stream()), "group_norm_affine")
+    if PROFILER.active:
+        PROFILER.end()
+    return scale, shift
+
+
+def layer_norm(x2d, gamma, beta, eps=1e-5, out=None):
+    _need_cuda(x2d, "layer_norm")
+    M, Cc = x2d.shape
+    y = out if out is not None else torch.empty(M, Cc, dtype=torch.float16, device=x2d.device)
+    if PROFILER.active:
+        PROFILER.begin("layer_norm", None)
+    check(lib().sdk_layer_norm(_ptr(x2d), _ptr(y), M, Cc, x2d.stride(0), y.stride(0), _ptr(gamma), _ptr(beta),
+                               C.c_float(eps), _stream()), "layer_norm")
+    if PROFILER.active:
+        PROFILER.end()
+    return y
+
+
+# --------------------------------------------------------------------------- attention
+
+def attention(q, k, v, *, batch, heads, nq, nk, head_dim, scale, out=None):
+    """q/k/v: 2-D fp16 views [batch*n, ld] (head h at columns h*head_dim...)."""
+    for t, n in ((q, "q"), (k, "k"), (v, "v")):
+        _need_cuda(t, "attention " + n)
+    if out is None:
+        out = torch.empty(batch * nq, heads * head_dim, dtype=torch.float16, device=q.device)
+    a = AttentionArgs()
+    a.q, a.k, a.v, a.o = q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr()
+    a.q_ld, a.k_ld, a.v_ld, a.o_ld = q.stride(0), k.stride(0), v.stride(0), out.stride(0)
+    a.batch, a.heads, a.nq, a.nk, a.head_dim, a.scale = batch, heads, nq, nk, head_dim, scale
+    if PROFILER.active:
+        PROFILER.begin("attention", (batch, heads, nq, nk, head_dim))
+    check(lib().sdk_attention(C.byref(a), _stream()), "attention")
+    if PROFILER.active:
+        PROFILER.end()
+    return out
+
+
+# --------------------------------------------------------------------------- sampler glue
+
+def timestep_embedding(t: torch.Tensor, freqs: torch.Tensor, dim: int):
+    _need_cuda(t, "timestep_embedding", torch.int64)
+    out = torch.empty(t.shape[0], dim, dtype=torch.float16, device=t.device)
+    check(lib().sdk_timestep_embedding(_ptr(t), _ptr(freqs), _ptr(out), t.shape[0], dim, _stream()),
+          "timestep_embedding")
+    return out
+
+
+def nchw_to_nhwc(x: torch.Tensor, c_pad: int, scale: float = 1.0):
+    _need_cuda(x, "nchw_to_nhwc", torch.float32)
+    x = x.contiguous()
+    B, Cc, H, W = x.shape
+    y = torch.empty(B, H, W, c_pad, dtype=torch.float16, device=x.device)
+    check(lib().sdk_nchw_to_nhwc(_ptr(x), _ptr(y), B, Cc, H * W, c_pad, C.c_float(scale), _stream()),
+          "nchw_to_nhwc")
+    return y
+
+
+def ddim_step(x, e, sc: dict, noise=None, e_uncond=None, guidance=1.0, v_param=None, x_prev=None, pred_x0=None,
+              temperature=1.0):
+    """Fused DDIM update; ``sc`` holds the fp32 scalars (sampler.DDIMSampler computes them)."""
+    _need_cuda(x, "ddim_step", torch.float32)
+    _need_cuda(e, "ddim_step", torch.float32)
+    a = DdimArgs()
+    xp = x_prev if x_prev is not None else torch.empty_like(x)
+    p0 = pred_x0 if pred_x0 is not None else torch.empty_like(x)
+    a.x, a.e, a.x_prev, a.pred_x0 = x.data_ptr(), e.data_ptr(), xp.data_ptr(), p0.data_ptr()
+    a.e_uncond = e_uncond.data_ptr() if e_uncond is not None else None
+    a.noise = noise.data_ptr() if noise is not None else None
+    a.n = x.numel()
+    a.sqrt_one_minus_at = float(sc["sqrt_one_minus_at"])
+    a.sqrt_at = float(sc["sqrt_at"])
+    a.dir_coef = float(sc["dir_coef"])
+    a.sqrt_a_prev = float(sc["sqrt_a_prev"])
+    a.sigma = float(sc["sigma"])
+    a.temperature = float(temperature)
+    a.guidance = float(guidance)
+    if v_param is not None:
+        a.v_param = 1
+        a.v_sqrt_a, a.v_sqrt_1ma = float(v_param[0]), float(v_param[1])
+    check(lib().sdk_ddim_step(C.byref(a), _stream()), "ddim_step")
+    return xp, p0
+
+
+def ddpm_step(x, eps, noise, inv_sqrt_alpha, coef, sigma, out=None):
+    _need_cuda(x, "ddpm_step", torch.float32)
+    y = out if out is not None else torch.empty_like(x)
+    check(lib().sdk_ddpm_step(_ptr(x), _ptr(eps), _ptr(noise), _ptr(y), x.numel(), C.c_float(inv_sqrt_alpha),
+                              C.c_float(coef), C.c_float(sigma), _stream()), "ddpm_step")
+    return y
+
+
+# --------------------------------------------------------------------------- profiling hooks
+
+class _Profiler:
+    """Optional per-launch HIP-event timing on the launch stream (bench roofline leg)."""
+
+    def __init__(self):
+        self.active = False
+        self.records = []
+        self._cur = None
+
+    def start(self):
+        self.records = []
+        self.active = True
+
+    def stop(self):
+        self.active = False
+
+    def begin(self, kind, info):
+        s = torch.cuda.current_stream()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        flops = info.flops if isinstance(info, ConvPlanInfo) else None
+        if kind == "attention" and info is not None:
+            b, h, nq, nk, d = info
+            flops = 4.0 * b * h * nq * nk * d
+        variant = info.variant if isinstance(info, ConvPlanInfo) else None
+        self._cur = (kind, variant, flops, e0)
+
+    def end(self):
+        s = torch.cuda.current_stream()
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record(s)
+        kind, variant, flops, e0 = self._cur
+        self.records.append((kind, variant, flops, e0, e1))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for kind, variant, flops, e0, e1 in self.records:
+            key = kind if variant is None else f"{kind}:{variant}"
+            d = out.setdefault(key, {"launches": 0, "ms": 0.0, "flops": 0.0})
+            d["launches"] += 1
+            d["ms"] += e0.elapsed_time(e1)
+            d["flops"] += flops or 0.0
+        return out
+
+
+PROFILER = _Profiler()
