@@ -127,6 +127,12 @@ typedef struct {
 int64_t sdk_group_norm_workspace(int32_t batch, int32_t hw, int32_t channels);
 int sdk_group_norm_affine(const sdk_group_norm_args* a, sdk_stream_t stream);
 
+/* y = silu?(x*scale + shift) with the scale/shift of sdk_group_norm_affine; writes the
+ * (possibly 2-source) input contiguous [batch*hw][ld_y].  Used in front of 3x3 convs,
+ * where a per-tap prologue would repeat the transform 9x (GroupNorm32 + nn.SiLU,
+ * openai_model/model.py:178-181,202-205,528-530; Unet/unet.py:116-125; encoder.py:205-206). */
+int sdk_group_norm_apply(const sdk_group_norm_args* a, int32_t silu, void* y, int32_t ld_y, sdk_stream_t stream);
+
 /* ---------------------------------------------------------------- LayerNorm
  * y = (x - mean) * rstd * gamma + beta over the last dim, fp16 in/out, fp32 math.
  * Replaces nn.LayerNorm norm1/2/3 (openai_model/attention.py:216-218,251-253).

@@ -142,7 +142,8 @@ class Decoder(nn.Module):
             raise NotImplementedError("sd_amd: give_pre_end is not on the SD path")
         if self.tanh_out:
             raise NotImplementedError("sd_amd: tanh_out is not on the SD path")
-        return ops.conv2d(self._pc_out, h, gn=gn_stats(self.norm_out, h), silu=True, out_mode=ops.OUT_NCHW_F32)
+        ha = ops.group_norm_apply(h, gn_stats(self.norm_out, h), silu=True)
+        return ops.conv2d(self._pc_out, ha, out_mode=ops.OUT_NCHW_F32)
 
     @torch.no_grad()
     def forward(self, z):

@@ -95,10 +95,10 @@ class ResnetBlock(nn.Module):
     def _run(self, x, temb=None):
         if temb is not None:
             raise NotImplementedError("sd_amd: the VAE ResnetBlock path has no timestep embedding")
-        h = ops.conv2d(self._pc1, x, gn=gn_stats(self.norm1, x), silu=True)
-        gn2 = gn_stats(self.norm2, h)
+        h = ops.conv2d(self._pc1, ops.group_norm_apply(x, gn_stats(self.norm1, x), silu=True))
+        ha = ops.group_norm_apply(h, gn_stats(self.norm2, h), silu=True)
         if self._mode == "identity":
-            return ops.conv2d(self._pc2, h, gn=gn2, silu=True, residual=x)
+            return ops.conv2d(self._pc2, ha, residual=x)
         if self._mode == "fused":
-            return ops.conv2d(self._pc2, h, gn=gn2, silu=True, seg2=(x, None, False))
-        return ops.conv2d(self._pc2, h, gn=gn2, silu=True, residual=ops.conv2d(self._pcs, x))
+            return ops.conv2d(self._pc2, ha, seg2=(x, None, False))
+        return ops.conv2d(self._pc2, ha, residual=ops.conv2d(self._pcs, x))

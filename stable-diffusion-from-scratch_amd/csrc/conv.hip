@@ -128,7 +128,7 @@ __device__ __forceinline__ void transform_a(const Params& p, const RowCtx& rc, i
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float x = (float)v[j] * sc[j] + sh[j];
-        if (s.silu) x = silu_f(x);
+        if (s.silu) x = x * __builtin_amdgcn_rcpf(1.0f + __expf(-x));
         v[j] = (half_t)x;
       }
     } else {
@@ -293,18 +293,24 @@ __global__ void __launch_bounds__(NT, 2) conv_igemm_kernel(Params p) {
     half_t* ct = smem;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      // a 32-row MFMA block never straddles two images (hw_out % 32 == 0 is required for row_bias)
+      // a 32-row MFMA block straddles two images only when ho*wo % 32 != 0 (4x4 levels)
       const int mblk = m0 + wm * 64 + i * 32;
       const int bidx = min(mblk, p.M - 1) / p.hw_out;
+      const bool uniform_b = (p.hw_out % 32) == 0;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int n = n0 + wn * 64 + j * 32 + fr;
         float add = bn[j];
-        if (p.row_bias && n < p.N) add += p.row_bias[(size_t)bidx * p.rb_ld + n];
+        if (p.row_bias && n < p.N && uniform_b) add += p.row_bias[(size_t)bidx * p.rb_ld + n];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int rl = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
-          ct[rl * CT_LD + wn * 64 + j * 32 + fr] = (half_t)(acc[i][j][r] + add);
+          float v = acc[i][j][r] + add;
+          if (p.row_bias && n < p.N && !uniform_b) {
+            const int m = min(m0 + rl, p.M - 1);
+            v += p.row_bias[(size_t)(m / p.hw_out) * p.rb_ld + n];
+          }
+          ct[rl * CT_LD + wn * 64 + j * 32 + fr] = (half_t)v;
         }
       }
     }
@@ -439,8 +445,6 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
       return fail(SDK_EINVAL, "conv2d: fp16 NHWC output needs cout/out_ld/res_ld multiples of 8");
   }
   if (a->out_mode == SDK_OUT_GEGLU_F16 && (a->cout % 64)) return fail(SDK_EINVAL, "conv2d: GEGLU cout % 64");
-  if (a->row_bias && (p.hw_out % 32) && a->out_mode == SDK_OUT_NHWC_F16)
-    return fail(SDK_EINVAL, "conv2d: row_bias needs ho*wo % 32 == 0");
   p.kt_total = kt;
   p.W = (const half_t*)a->weight; p.ldw = a->k_total;
   p.bias = a->bias; p.row_bias = a->row_bias; p.rb_ld = a->row_bias_ld;
@@ -454,7 +458,7 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
     // fill the 256 CUs x 2 resident workgroups; keep >= 8 K tiles per split
     while (tiles * split < 384 && kt / (split * 2) >= 8 && split < 16) split *= 2;
   }
-  if (a->out_mode == SDK_OUT_GEGLU_F16) split = 1;
+  if (a->out_mode == SDK_OUT_GEGLU_F16 || a->cout % 8) split = 1;
   if (split > kt) split = kt;
   p.kt_per_split = (kt + split - 1) / split;
   split = (kt + p.kt_per_split - 1) / p.kt_per_split;
@@ -468,7 +472,7 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
     info->flops = 2.0 * p.M * (double)p.N * kreal;
   }
   if (split > 1) {
-    if (a->cout % 8) return fail(SDK_EINVAL, "conv2d: split-K needs cout % 8 == 0");
+    if (a->cout % 8) return fail(SDK_EINVAL, "conv2d: split-K needs cout % 8 == 0 (pass split_k = 1)");
     p.partial = a->workspace;
   }
   return SDK_OK;

@@ -144,6 +144,37 @@ __global__ void __launch_bounds__(64) gn_finalize_kernel(const half_t* s0, const
   }
 }
 
+// GroupNorm apply (+ SiLU): y = silu?(x*scale[b,c] + shift[b,c]), 8 channels per thread,
+// 16-B loads/stores, reads the (optional) 2-source concat and writes it contiguous.
+// Applying the per-tap prologue inside a 3x3 implicit GEMM would repeat this
+// VALU work 9x per element; one streaming pass is HBM-bound instead.
+__global__ void __launch_bounds__(256) gn_apply_kernel(const half_t* s0, const half_t* s1, int c_split, int ld0,
+                                                       int ld1, int hw, int channels, const float* scale,
+                                                       const float* shift, int silu, half_t* y, int ldy,
+                                                       int64_t nvec) {
+  const int c8 = channels / 8;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nvec; e += stride) {
+    const int64_t pix = e / c8;
+    const int c = (int)(e - pix * c8) * 8;
+    const int b = (int)(pix / hw);
+    h8 v = load_px(s0, s1, c_split, ld0, ld1, (size_t)pix, c);
+    const f4* ps = reinterpret_cast<const f4*>(scale + (size_t)b * channels + c);
+    const f4* pt = reinterpret_cast<const f4*>(shift + (size_t)b * channels + c);
+    const f4 sa = ps[0], sb = ps[1], ta = pt[0], tb = pt[1];
+    const float sc[8] = {sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3]};
+    const float sh[8] = {ta[0], ta[1], ta[2], ta[3], tb[0], tb[1], tb[2], tb[3]};
+    h8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float x = (float)v[j] * sc[j] + sh[j];
+      if (silu) x = x * __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+      o[j] = (half_t)x;
+    }
+    *reinterpret_cast<h8*>(y + (size_t)pix * ldy + c) = o;
+  }
+}
+
 // LayerNorm: one wave per row, row cached in registers (cols <= 64*8*MAXV).
 constexpr int LN_MAXV = 4;
 __global__ void __launch_bounds__(256) layer_norm_kernel(const half_t* x, half_t* y, int rows, int cols, int ldx,
@@ -229,6 +260,22 @@ extern "C" int sdk_group_norm_affine(const sdk_group_norm_args* a, sdk_stream_t 
                      (const half_t*)a->src1, a->c_split, a->ld0, a->ld1, a->hw, a->channels, a->groups, g,
                      (const float2*)a->workspace, a->eps, a->gamma, a->beta, a->scale, a->shift);
   return check_launch("gn_finalize");
+}
+
+extern "C" int sdk_group_norm_apply(const sdk_group_norm_args* a, int32_t silu, void* y, int32_t ld_y,
+                                    sdk_stream_t stream) {
+  if (!a || !a->src0 || !a->scale || !a->shift || !y) return fail(SDK_EINVAL, "group_norm_apply: null pointer");
+  if (a->channels % 8 || a->c_split % 8 || a->c_split <= 0 || a->c_split > a->channels || ld_y % 8 ||
+      ld_y < a->channels)
+    return fail(SDK_EINVAL, "group_norm_apply: channels/c_split/ld_y must be multiples of 8");
+  if (a->c_split < a->channels && !a->src1) return fail(SDK_EINVAL, "group_norm_apply: concat without src1");
+  const int64_t nvec = (int64_t)a->batch * a->hw * (a->channels / 8);
+  if (nvec <= 0) return SDK_OK;
+  const int blocks = (int)std::min<int64_t>((nvec + 255) / 256, 8192);
+  hipLaunchKernelGGL(gn_apply_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const half_t*)a->src0,
+                     (const half_t*)a->src1, a->c_split, a->ld0, a->ld1, a->hw, a->channels, a->scale, a->shift,
+                     silu, (half_t*)y, ld_y, nvec);
+  return check_launch("gn_apply");
 }
 
 extern "C" int sdk_layer_norm(const void* x, void* y, int32_t rows, int32_t cols, int32_t ld_x, int32_t ld_y,

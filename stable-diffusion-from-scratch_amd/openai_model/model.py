@@ -5,10 +5,10 @@ keys) and ``UNetModel.forward(x, timesteps=None, context=None, y=None)`` →
 ``[N, out_ch, H, W]`` in ``x.dtype``.  Internally activations are NHWC fp16,
 every conv/linear/norm/attention runs in libsdk_amd.so:
 
-* ResBlock = GN-stats → conv3x3 (GN+SiLU prologue, bias + timestep-embedding
-  broadcast epilogue) → GN-stats → conv3x3 (GN+SiLU prologue, + skip): the 1x1
-  skip projection is fused as a second K segment of the same GEMM, the identity
-  skip as the residual epilogue.  Each ResBlock runs ONCE (the reference's
+* ResBlock = GN stats → GN-apply+SiLU (one streaming pass) → conv3x3 (bias +
+  timestep-embedding broadcast epilogue) → GN stats → GN-apply+SiLU → conv3x3
+  (+ skip): the 1x1 skip projection is fused as a second K segment of the same
+  GEMM, the identity skip as the residual epilogue.  Each ResBlock runs ONCE (the reference's
   ``checkpoint(..., flag=False)`` evaluates it twice, ``openai_model/utils.py:217-221``).
 * The skip concat ``torch.cat([h, hs.pop()], 1)`` is never materialised: the
   next block reads both tensors as one K range.
@@ -138,15 +138,15 @@ class ResBlock(TimestepBlock):
                 self._pc_skip = ops.PackedConv([(sk.weight, self.channels)], sk.bias, device=dev)
 
     def _run(self, x, emb_all, emb_off):
-        gn1 = self.in_layers[0].stats(x)
-        h = ops.conv2d(self._pc1, x, gn=gn1, silu=True, row_bias=(emb_all, emb_off))
-        gn2 = self.out_layers[0].stats(h)
+        xa = ops.group_norm_apply(x, self.in_layers[0].stats(x), silu=True)
+        h = ops.conv2d(self._pc1, xa, row_bias=(emb_all, emb_off))
+        ha = ops.group_norm_apply(h, self.out_layers[0].stats(h), silu=True)
         if self._skip_mode == "identity":
-            return ops.conv2d(self._pc2, h, gn=gn2, silu=True, residual=x)
+            return ops.conv2d(self._pc2, ha, residual=x)
         if self._skip_mode == "fused":
-            return ops.conv2d(self._pc2, h, gn=gn2, silu=True, seg2=(x, None, False))
+            return ops.conv2d(self._pc2, ha, seg2=(x, None, False))
         skip = ops.conv2d(self._pc_skip, x)
-        return ops.conv2d(self._pc2, h, gn=gn2, silu=True, residual=skip)
+        return ops.conv2d(self._pc2, ha, residual=skip)
 
 
 class UNetModel(nn.Module):
@@ -342,6 +342,6 @@ class UNetModel(nn.Module):
         h = self.middle_block._run(h, st)
         for module in self.output_blocks:
             h = module._run((h, hs.pop()), st)
-        gn = self.out[0].stats(h)
-        out = ops.conv2d(self._pc_out, h, gn=gn, silu=True, out_mode=ops.OUT_NCHW_F32)
+        ha = ops.group_norm_apply(h, self.out[0].stats(h), silu=True)
+        out = ops.conv2d(self._pc_out, ha, out_mode=ops.OUT_NCHW_F32)
         return out if x.dtype == torch.float32 else out.to(x.dtype)

@@ -78,9 +78,9 @@ def src_shape(x):
 def _fill_src(s: "_lib.ConvSrc", x, ksize, stride, pad, upsample, gn, silu):
     a, b = _as_pair(x)
     _need_cuda(a, "conv2d")
-    if a.stride(-1) != 1:
-        raise ValueError("sd_amd.conv2d: source channels must be contiguous")
     B, H, W, C0 = a.shape
+    if a.stride(3) != 1 or (H > 1 and a.stride(1) != W * a.stride(2)) or (B > 1 and a.stride(0) != H * a.stride(1)):
+        raise ValueError("sd_amd.conv2d: source must be NHWC with contiguous channels and a uniform pixel stride")
     s.src0 = a.data_ptr()
     s.ld0 = a.stride(2) if a.dim() == 4 else a.stride(1)
     if b is not None:
@@ -227,6 +227,39 @@ def linear(pc: PackedConv, x2d, *, silu=False, residual=None, out_mode=OUT_NHWC_
 
 # --------------------------------------------------------------------------- normalisation
 
+def _gn_args(x):
+    a0, a1 = _as_pair(x)
+    _need_cuda(a0, "group_norm")
+    B, H, W, Ch = src_shape(x)
+    args = GroupNormArgs()
+    args.src0 = a0.data_ptr()
+    args.ld0 = a0.stride(2)
+    if a1 is not None:
+        args.src1 = a1.data_ptr()
+        args.ld1 = a1.stride(2)
+    args.c_split = a0.shape[-1]
+    args.batch, args.hw, args.channels = B, H * W, Ch
+    return args, (B, H, W, Ch), a0.device
+
+
+def group_norm_apply(x, gn, silu=True, out=None):
+    """y = silu?(x*scale + shift) — the normalised (possibly concatenated) input, contiguous NHWC."""
+    args, (B, H, W, Ch), dev = _gn_args(x)
+    args.scale, args.shift = gn[0].data_ptr(), gn[1].data_ptr()
+    y = out if out is not None else torch.empty(B, H, W, Ch, dtype=torch.float16, device=dev)
+    if PROFILER.active:
+        PROFILER.begin("gn_apply", None)
+    check(lib().sdk_group_norm_apply(C.byref(args), 1 if silu else 0, _ptr(y), Ch, _stream()), "group_norm_apply")
+    if PROFILER.active:
+        PROFILER.end()
+    return y
+
+
+def group_norm_silu(x, gamma, beta, eps, groups=32):
+    """GroupNorm + SiLU materialised once (stats pass + apply pass) — the input of a 3x3 conv."""
+    return group_norm_apply(x, group_norm_affine(x, gamma, beta, eps, groups), silu=True)
+
+
 def group_norm_affine(x, gamma, beta, eps, groups=32):
     """Per-(batch, channel) (scale, shift) fp32 [B, C] of GroupNorm(x) for the conv prologue."""
     a0, a1 = _as_pair(x)
@@ -314,6 +347,11 @@ def ddim_step(x, e, sc: dict, noise=None, e_uncond=None, guidance=1.0, v_param=N
     """Fused DDIM update; ``sc`` holds the fp32 scalars (sampler.DDIMSampler computes them)."""
     _need_cuda(x, "ddim_step", torch.float32)
     _need_cuda(e, "ddim_step", torch.float32)
+    x, e = x.contiguous(), e.contiguous()
+    if e_uncond is not None:
+        e_uncond = e_uncond.contiguous()
+    if noise is not None:
+        noise = noise.contiguous()
     a = DdimArgs()
     xp = x_prev if x_prev is not None else torch.empty_like(x)
     p0 = pred_x0 if pred_x0 is not None else torch.empty_like(x)

@@ -211,3 +211,19 @@ def test_nchw_to_nhwc(ops):
     ref = torch.zeros(3, 17, 9, 8)
     ref[..., :4] = (x * 0.5).permute(0, 2, 3, 1)
     assert torch.equal(y.cpu(), ref.half())
+
+
+@pytest.mark.parametrize("silu", [True, False])
+def test_group_norm_apply_concat(ops, silu):
+    B, H, W, C1, C2 = 2, 16, 16, 640, 320
+    a, b2 = _rand(B, H, W, C1, seed=15), _rand(B, H, W, C2, seed=16)
+    gamma, beta = torch.rand(C1 + C2) + 0.5, torch.randn(C1 + C2) * 0.1
+    src = (a.to(DEV), b2.to(DEV))
+    gn = ops.group_norm_affine(src, gamma.to(DEV), beta.to(DEV), 1e-5)
+    y = ops.group_norm_apply(src, gn, silu=silu)
+    xr = torch.cat([a, b2], -1).float().permute(0, 3, 1, 2)
+    ref = F.group_norm(xr, 32, gamma, beta, 1e-5)
+    if silu:
+        ref = F.silu(ref)
+    assert y.shape == (B, H, W, C1 + C2)
+    assert rel_l2(y, ref.permute(0, 2, 3, 1)) < 1e-3
