@@ -99,7 +99,7 @@ typedef struct {
   int32_t split_k;
   int32_t grid_tiles;
   int64_t workspace_bytes;
-  int32_t variant;         /* kernel variant id (index into sdk_kernel_name) */
+  int32_t variant;         /* kernel variant id (sdk_kernel_name); split_k > 1 adds splitk_reduce_kernel */
   double flops;            /* algorithmic 2*M*N*K over the unpadded K */
 } sdk_conv_plan_info;
 

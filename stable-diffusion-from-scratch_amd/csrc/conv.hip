@@ -18,6 +18,9 @@
 // stages the fp16 tile through LDS and writes it with 16-B coalesced stores
 // fused with the residual add.  Low-parallelism shapes (the 16x16 / 8x8 UNet
 // levels) split K across workgroups into fp32 slabs reduced by a second kernel.
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.h"
 
 namespace sdk {
@@ -44,7 +47,7 @@ struct Params {
   int nseg, kt_total;
   int M, N, Npad, batch, ho, wo, hw_out;
   const half_t* W;
-  int ldw;
+  int ldw, wrows;       // packed weight rows (>= N); reads beyond are clamped
   const float* bias;
   const float* row_bias;
   int rb_ld;
@@ -55,6 +58,7 @@ struct Params {
   float* partial;       // split-K slabs [split][M][Npad]
   int split, kt_per_split;
   int tiles_m, tiles_n;
+  int variant;          // 0: register-staged 128x128 (A transforms); 2/3/4: LDS-DMA 256x256 / 256x128 / 128x128
 };
 
 __device__ __forceinline__ int swz(int row, int chunk) {   // element offset inside a [128][64] tile
@@ -138,6 +142,135 @@ __device__ __forceinline__ void transform_a(const Params& p, const RowCtx& rc, i
   }
 }
 
+
+// ---------------------------------------------------------------------- shared epilogue
+// acc[i][j] (32x32 MFMA tile) element r of lane (fr = lane&31, fh = lane>>5):
+//   row = m_w + i*32 + (r&3) + 8*(r>>2) + 4*fh, col = n_w + j*32 + fr   (block-local)
+// LDS `smem` must be free (all waves past their last LDS read) on entry.
+template <int FM, int FN, int TBM, int TBN, int TNT>
+__device__ __forceinline__ void epilogue(const Params& p, f16v (&acc)[FM][FN], half_t* smem, int m0, int n0, int m_w,
+                                         int n_w, int split_idx) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int fr = lane & 31, fh = lane >> 5;
+  constexpr int CLD = TBN + 8;
+  if (p.split > 1) {
+    float* slab = p.partial + (size_t)split_idx * p.M * p.Npad;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + m_w + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+          const int n = n0 + n_w + j * 32 + fr;
+          if (m < p.M) slab[(size_t)m * p.Npad + n] = acc[i][j][r];
+        }
+    return;
+  }
+  const int mode = p.out_mode;
+  if (mode == SDK_OUT_GEGLU_F16) {
+    // weight rows of each 64-wide column pair: [x (32) | gate (32)] -> output col = (n_w + j*32)/2 + fr
+    static_assert(FN % 2 == 0, "GEGLU needs an even number of 32-col tiles per wave");
+#pragma unroll
+    for (int jp = 0; jp < FN / 2; ++jp) {
+      const int nx = n0 + n_w + jp * 64 + fr, ng = nx + 32;
+      const float bx = (p.bias && nx < p.N) ? p.bias[nx] : 0.f, bg = (p.bias && ng < p.N) ? p.bias[ng] : 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rl = m_w + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+          const float x = acc[i][2 * jp][r] + bx, g = acc[i][2 * jp + 1][r] + bg;
+          smem[rl * CLD + n_w / 2 + jp * 32 + fr] = (half_t)(x * gelu_erf(g));
+        }
+    }
+    __syncthreads();
+    constexpr int OW = TBN / 2;
+    const int ncol0 = n0 / 2;
+    half_t* out = reinterpret_cast<half_t*>(p.out);
+    for (int e = tid; e < TBM * (OW / 8); e += TNT) {
+      const int rl = e / (OW / 8), c8 = (e - rl * (OW / 8)) * 8;
+      const int m = m0 + rl, n = ncol0 + c8;
+      if (m >= p.M || n >= p.N / 2) continue;
+      h8 v = *reinterpret_cast<const h8*>(smem + rl * CLD + c8);
+      if (p.res) {
+        h8 rr = ldg16(p.res + (size_t)m * p.res_ld + n);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = (half_t)((float)v[q] + (float)rr[q]);
+      }
+      *reinterpret_cast<h8*>(out + (size_t)m * p.out_ld + n) = v;
+    }
+    return;
+  }
+  float bn[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = n0 + n_w + j * 32 + fr;
+    bn[j] = (p.bias && n < p.N) ? p.bias[n] : 0.f;
+  }
+  if (mode == SDK_OUT_NHWC_F16) {
+    const bool uniform_b = (p.hw_out % 32) == 0;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int mblk = m0 + m_w + i * 32;
+      const int bidx = min(mblk, p.M - 1) / p.hw_out;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = n0 + n_w + j * 32 + fr;
+        float add = bn[j];
+        if (p.row_bias && n < p.N && uniform_b) add += p.row_bias[(size_t)bidx * p.rb_ld + n];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rl = m_w + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+          float v = acc[i][j][r] + add;
+          if (p.row_bias && n < p.N && !uniform_b) {
+            const int m = min(m0 + rl, p.M - 1);
+            v += p.row_bias[(size_t)(m / p.hw_out) * p.rb_ld + n];
+          }
+          smem[rl * CLD + n_w + j * 32 + fr] = (half_t)v;
+        }
+      }
+    }
+    __syncthreads();
+    half_t* out = reinterpret_cast<half_t*>(p.out);
+    for (int e = tid; e < TBM * (TBN / 8); e += TNT) {
+      const int rl = e / (TBN / 8), c8 = (e - rl * (TBN / 8)) * 8;
+      const int m = m0 + rl, n = n0 + c8;
+      if (m >= p.M || n >= p.N) continue;
+      h8 v = *reinterpret_cast<const h8*>(smem + rl * CLD + c8);
+      if (p.res) {
+        h8 rr = ldg16(p.res + (size_t)m * p.res_ld + n);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = (half_t)((float)v[q] + (float)rr[q]);
+      }
+      *reinterpret_cast<h8*>(out + (size_t)m * p.out_ld + n) = v;
+    }
+    return;
+  }
+  // fp32 outputs (small: time-embedding projections, final 4/3-channel convs)
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + n_w + j * 32 + fr;
+      if (n >= p.N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + m_w + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+        if (m >= p.M) continue;
+        const int b = m / p.hw_out;
+        float v = acc[i][j][r] + bn[j];
+        if (p.row_bias) v += p.row_bias[(size_t)b * p.rb_ld + n];
+        if (p.res) v += (float)p.res[(size_t)m * p.res_ld + n];
+        float* out = reinterpret_cast<float*>(p.out);
+        if (mode == SDK_OUT_NCHW_F32)
+          out[((size_t)b * p.N + n) * p.hw_out + (m - b * p.hw_out)] = v;
+        else
+          out[(size_t)m * p.out_ld + n] = v;
+      }
+    }
+}
+
 __global__ void __launch_bounds__(NT, 2) conv_igemm_kernel(Params p) {
   __shared__ __attribute__((aligned(16))) half_t smem[4 * TILE_H];   // A0 A1 B0 B1 = 64 KiB
   half_t* As = smem;
@@ -165,7 +298,7 @@ __global__ void __launch_bounds__(NT, 2) conv_igemm_kernel(Params p) {
   }
   const half_t* wrow[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) wrow[i] = p.W + (size_t)(n0 + lrow + 32 * i) * p.ldw + chunk * 8;
+  for (int i = 0; i < 4; ++i) wrow[i] = p.W + (size_t)min(n0 + lrow + 32 * i, p.wrows - 1) * p.ldw + chunk * 8;
 
   f16v acc[2][2];
 #pragma unroll
@@ -233,127 +366,283 @@ __global__ void __launch_bounds__(NT, 2) conv_igemm_kernel(Params p) {
     __syncthreads();
   }
 
-  // ------------------------------------------------------------------ epilogue
-  // acc[i][j] element r: row = wm*64 + i*32 + (r&3) + 8*(r>>2) + 4*fh, col = wn*64 + j*32 + fr
-  if (p.split > 1) {
-    float* slab = p.partial + (size_t)blockIdx.y * p.M * p.Npad;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
-          const int n = n0 + wn * 64 + j * 32 + fr;
-          if (m < p.M) slab[(size_t)m * p.Npad + n] = acc[i][j][r];
-        }
-    return;
-  }
-
-  const int mode = p.out_mode;
-  if (mode == SDK_OUT_GEGLU_F16) {
-    // weight rows of this wave: [x (32) | gate (32)] -> output col = n0/2 + wn*32 + fr
-    half_t* ct = smem;   // [128][CT_LD], only 64 columns used
-    const int nx = n0 + wn * 64 + fr, ng = nx + 32;
-    const float bx = (p.bias && nx < p.N) ? p.bias[nx] : 0.f, bg = (p.bias && ng < p.N) ? p.bias[ng] : 0.f;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int rl = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
-        const float x = acc[i][0][r] + bx, g = acc[i][1][r] + bg;
-        ct[rl * CT_LD + wn * 32 + fr] = (half_t)(x * gelu_erf(g));
-      }
-    __syncthreads();
-    const int outw = BN / 2, ncol0 = n0 / 2;
-    half_t* out = reinterpret_cast<half_t*>(p.out);
-    for (int e = tid; e < BM * (outw / 8); e += NT) {
-      const int rl = e / (outw / 8), c8 = (e - rl * (outw / 8)) * 8;
-      const int m = m0 + rl, n = ncol0 + c8;
-      if (m >= p.M || n >= p.N / 2) continue;
-      h8 v = *reinterpret_cast<const h8*>(ct + rl * CT_LD + c8);
-      if (p.res) {
-        h8 rr = ldg16(p.res + (size_t)m * p.res_ld + n);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (half_t)((float)v[j] + (float)rr[j]);
-      }
-      *reinterpret_cast<h8*>(out + (size_t)m * p.out_ld + n) = v;
-    }
-    return;
-  }
-
-  float bn[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int n = n0 + wn * 64 + j * 32 + fr;
-    bn[j] = (p.bias && n < p.N) ? p.bias[n] : 0.f;
-  }
-
-  if (mode == SDK_OUT_NHWC_F16) {
-    half_t* ct = smem;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      // a 32-row MFMA block straddles two images only when ho*wo % 32 != 0 (4x4 levels)
-      const int mblk = m0 + wm * 64 + i * 32;
-      const int bidx = min(mblk, p.M - 1) / p.hw_out;
-      const bool uniform_b = (p.hw_out % 32) == 0;
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int n = n0 + wn * 64 + j * 32 + fr;
-        float add = bn[j];
-        if (p.row_bias && n < p.N && uniform_b) add += p.row_bias[(size_t)bidx * p.rb_ld + n];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int rl = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
-          float v = acc[i][j][r] + add;
-          if (p.row_bias && n < p.N && !uniform_b) {
-            const int m = min(m0 + rl, p.M - 1);
-            v += p.row_bias[(size_t)(m / p.hw_out) * p.rb_ld + n];
-          }
-          ct[rl * CT_LD + wn * 64 + j * 32 + fr] = (half_t)v;
-        }
-      }
-    }
-    __syncthreads();
-    half_t* out = reinterpret_cast<half_t*>(p.out);
-    for (int e = tid; e < BM * (BN / 8); e += NT) {
-      const int rl = e >> 4, c8 = (e & 15) * 8;
-      const int m = m0 + rl, n = n0 + c8;
-      if (m >= p.M || n >= p.N) continue;
-      h8 v = *reinterpret_cast<const h8*>(ct + rl * CT_LD + c8);
-      if (p.res) {
-        h8 rr = ldg16(p.res + (size_t)m * p.res_ld + n);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (half_t)((float)v[j] + (float)rr[j]);
-      }
-      *reinterpret_cast<h8*>(out + (size_t)m * p.out_ld + n) = v;
-    }
-    return;
-  }
-
-  // fp32 outputs (small: time-embedding projections, final 4/3-channel convs)
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = n0 + wn * 64 + j * 32 + fr;
-      if (n >= p.N) continue;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
-        if (m >= p.M) continue;
-        const int b = m / p.hw_out;
-        float v = acc[i][j][r] + bn[j];
-        if (p.row_bias) v += p.row_bias[(size_t)b * p.rb_ld + n];
-        if (p.res) v += (float)p.res[(size_t)m * p.res_ld + n];
-        float* out = reinterpret_cast<float*>(p.out);
-        if (mode == SDK_OUT_NCHW_F32)
-          out[((size_t)b * p.N + n) * p.hw_out + (m - b * p.hw_out)] = v;
-        else
-          out[(size_t)m * p.out_ld + n] = v;
-      }
-    }
+  const int m_w = wm * 64, n_w = wn * 64;
+  epilogue<2, 2, BM, BN, NT>(p, acc, smem, m0, n0, m_w, n_w, blockIdx.y);
 }
+
+
+
+// ---------------------------------------------------------------------- direct epilogue
+// Transposed accumulator (D^T = W A^T): lane (fr = lane&31, fh = lane>>5) owns output
+// pixel m = m0 + m_w + i*32 + fr; register group g (r = 4g..4g+3) of tile j holds the 4
+// consecutive channels n = n0 + n_w + j*32 + 8g + 4fh + (0..3) -> one 8-byte store per
+// group straight from registers (no LDS round trip, so the tile width is not bounded
+// by LDS), channel-contiguous in NHWC and pixel-contiguous for the NCHW fp32 output.
+template <int FM, int FN>
+__device__ __forceinline__ void epilogue_direct(const Params& p, f16v (&acc)[FM][FN], int m0, int n0, int m_w,
+                                                int n_w, int split_idx) {
+  const int lane = threadIdx.x & 63;
+  const int fr = lane & 31, fh = lane >> 5;
+  const int mode = p.out_mode;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int m = m0 + m_w + i * 32 + fr;
+    if (m >= p.M) continue;
+    const int b = m / p.hw_out;
+    if (p.split > 1) {
+      float* slab = p.partial + ((size_t)split_idx * p.M + m) * p.Npad;
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int n = n0 + n_w + j * 32 + 8 * g + 4 * fh;
+          f4 v = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+          *reinterpret_cast<f4*>(slab + n) = v;
+        }
+      continue;
+    }
+    if (mode == SDK_OUT_GEGLU_F16) {
+      half_t* out = reinterpret_cast<half_t*>(p.out) + (size_t)m * p.out_ld;
+#pragma unroll
+      for (int jp = 0; jp < FN / 2; ++jp)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int nx = n0 + n_w + jp * 64 + 8 * g + 4 * fh;      // x rows; gate rows = nx + 32
+          const int no = (n0 + n_w) / 2 + jp * 32 + 8 * g + 4 * fh; // output channel
+          if (no >= p.N / 2) continue;
+          h4 o;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float bx = p.bias ? p.bias[nx + q] : 0.f, bg = p.bias ? p.bias[nx + 32 + q] : 0.f;
+            const float x = acc[i][2 * jp][4 * g + q] + bx, gt = acc[i][2 * jp + 1][4 * g + q] + bg;
+            o[q] = (half_t)(x * gelu_erf(gt));
+          }
+          if (p.res) {
+            const h4 rr = *reinterpret_cast<const h4*>(p.res + (size_t)m * p.res_ld + no);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[q] = (half_t)((float)o[q] + (float)rr[q]);
+          }
+          *reinterpret_cast<h4*>(out + no) = o;
+        }
+      continue;
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n = n0 + n_w + j * 32 + 8 * g + 4 * fh;
+        if (n >= p.N) continue;                         // N % 4 == 0 for the fp16 modes
+        float v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = acc[i][j][4 * g + q];
+        if (p.bias) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] += (n + q < p.N) ? p.bias[n + q] : 0.f;
+        }
+        if (p.row_bias) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] += (n + q < p.N) ? p.row_bias[(size_t)b * p.rb_ld + n + q] : 0.f;
+        }
+        if (mode == SDK_OUT_NHWC_F16) {
+          h4 o;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) o[q] = (half_t)v[q];
+          if (p.res) {
+            const h4 rr = *reinterpret_cast<const h4*>(p.res + (size_t)m * p.res_ld + n);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[q] = (half_t)((float)o[q] + (float)rr[q]);
+          }
+          *reinterpret_cast<h4*>(reinterpret_cast<half_t*>(p.out) + (size_t)m * p.out_ld + n) = o;
+        } else {
+          float* out = reinterpret_cast<float*>(p.out);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (n + q >= p.N) continue;
+            float x = v[q];
+            if (p.res) x += (float)p.res[(size_t)m * p.res_ld + n + q];
+            if (mode == SDK_OUT_NCHW_F32)
+              out[((size_t)b * p.N + n + q) * p.hw_out + (m - b * p.hw_out)] = x;
+            else
+              out[(size_t)m * p.out_ld + n + q] = x;
+          }
+        }
+      }
+  }
+}
+
+// ---------------------------------------------------------------------- LDS-DMA kernel
+// A and W tiles are loaded straight into LDS with global_load_lds_dwordx4 (one
+// 1-KiB wave instruction = 8 rows x 128 B); the per-lane SOURCE address carries
+// the implicit-GEMM gather (pixel + tap + channel), the XOR swizzle of the LDS
+// image (rule: linear LDS destination, permuted source, same permutation on the
+// read) and zero padding (out-of-image taps read a 16-B zero page).  Two LDS
+// stages; the next tile's DMA is in flight across the barrier of the current
+// one (counted s_waitcnt vmcnt, raw s_barrier — never __syncthreads(), which
+// would drain it).  No VGPR staging, no A-side transform (GroupNorm+SiLU is
+// applied by gn_apply before 3x3 convs); every segment must be transform-free.
+__device__ __attribute__((aligned(16))) half_t g_zero_page[8];
+
+template <int BM_, int BN_, int WM_, int WN_>
+struct Cfg {
+  static constexpr int TBM = BM_, TBN = BN_, WM = WM_, WN = WN_;
+  static constexpr int NW = WM * WN, NT = NW * 64;
+  static constexpr int TM = TBM / WM, TN = TBN / WN;
+  static constexpr int FM = TM / 32, FN = TN / 32;
+  static constexpr int ROWS = TBM + TBN;                 // LDS rows (128 B) per stage
+  static constexpr int STAGE_H = ROWS * BK;              // halfs per stage
+  static constexpr int NINSTR = ROWS / 8;                // 1-KiB DMA pieces per stage
+  static constexpr int GPW = (NINSTR + NW - 1) / NW;     // pieces per wave (padded: the same count in
+                                                         // every wave keeps the vmcnt immediate exact)
+  static_assert(TBM % 8 == 0 && TBN % 8 == 0, "A/B boundary must align to an 8-row piece");
+  static constexpr int LDS_BYTES = 2 * STAGE_H * 2 + (GPW * NW > NINSTR ? 1024 : 0);  // + dummy slot
+  static_assert(LDS_BYTES <= 160 * 1024, "two stages must fit the 160 KiB LDS");
+};
+
+template <class CF>
+__global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_glds_kernel(Params p) {
+  extern __shared__ __attribute__((aligned(16))) half_t lds[];
+  constexpr int GPW = CF::GPW;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / CF::WN, wn = wave % CF::WN;
+  const int ntiles = p.tiles_m * p.tiles_n;
+  const int tile = xcd_remap(blockIdx.x, ntiles);
+  const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+  const int m0 = tm * CF::TBM, n0 = tn * CF::TBN;
+  const int kt0 = blockIdx.y * p.kt_per_split;
+  const int kt1 = min(p.kt_total, kt0 + p.kt_per_split);
+
+  // per-lane, per-instruction row context (fixed over the K loop): for A rows the
+  // output pixel (b, oy, ox); for W rows the weight row pointer.  Offsets into a
+  // source are 32-bit element counts (sources < 2^32 elements, checked on the host).
+  const int lrow = lane >> 3;
+  // A rows: ra[j] = (b << 16) | oy (oy = 0x7fff marks a row past M), rx[j] = ox;
+  // W rows: ra[j] = clamped weight row.  The swizzle chunk is recomputed per use.
+  int ra[GPW], rx[GPW];
+#pragma unroll
+  for (int j = 0; j < GPW; ++j) {
+    const int R = (j * CF::NW + wave) * 8 + lrow;           // stage row (instruction j*NW + wave)
+    if ((j * CF::NW + wave) >= CF::NINSTR) {                // padding piece
+      ra[j] = rx[j] = 0;
+    } else if ((j * CF::NW + wave) * 8 < CF::TBM) {         // A row (wave-uniform per j)
+      const int m = m0 + R;
+      const int mm = m < p.M ? m : 0;
+      const int b = mm / p.hw_out, rem = mm - b * p.hw_out;
+      const int oy = rem / p.wo;
+      ra[j] = (b << 16) | (m < p.M ? oy : 0x7fff);
+      rx[j] = rem - oy * p.wo;
+    } else {
+      ra[j] = min(n0 + R - CF::TBM, p.wrows - 1);          // weight row (clamped; cols >= N discarded)
+      rx[j] = 0;
+    }
+  }
+  const half_t* zero = g_zero_page;
+
+  // segment fields are read with constant indices only (uniform scalar selects): a
+  // dynamic index into the kernarg struct becomes vector loads whose s_waitcnt
+  // vmcnt(0) would drain the DMA in flight.
+  const int kt_b1 = p.nseg > 1 ? p.seg[1].kt_begin : 0x7fffffff;
+  auto stage = [&](int kt, int buf) {
+    const bool s1 = kt >= kt_b1;
+#define SEGF(f) (s1 ? p.seg[1].f : p.seg[0].f)
+    const int kt_begin = SEGF(kt_begin), tpt = SEGF(tiles_per_tap), ks = SEGF(ksize);
+    const int sh = SEGF(h), sw = SEGF(w), sstride = SEGF(stride), spad = SEGF(pad), sup = SEGF(upsample);
+    const int cin = SEGF(cin), csplit = SEGF(c_split), ld0 = SEGF(ld0), ld1 = SEGF(ld1), koff = SEGF(k_off);
+    const half_t* src0 = SEGF(src0);
+    const half_t* src1 = SEGF(src1);
+#undef SEGF
+    const int local = kt - kt_begin;
+    const int tap = local / tpt;
+    const int cbase = (local - tap * tpt) * BK;
+    const int ky = tap / ks, kx = tap - ky * ks;
+    const int kcol = koff + local * BK;
+    const unsigned lh = sup ? 2 * sh : sh, lw = sup ? 2 * sw : sw;
+    const int dy = ky - spad, dx = kx - spad;
+#pragma unroll
+    for (int j = 0; j < GPW; ++j) {
+      const int rbase = (j * CF::NW + wave) * 8;
+      const bool pad_piece = (j * CF::NW + wave) >= CF::NINSTR;
+      __attribute__((address_space(3))) void* dst =
+          (__attribute__((address_space(3))) void*)(pad_piece ? lds + 2 * CF::STAGE_H
+                                                              : lds + buf * CF::STAGE_H + rbase * BK);
+      const half_t* src;
+      const int rchunk = (lane & 7) ^ (((rbase >> 1) + (lrow >> 1)) & 7);
+      if (pad_piece) {
+        src = zero;
+      } else if (rbase < CF::TBM) {
+        const int c = cbase + rchunk * 8;
+        const int oy = ra[j] & 0xffff, bimg = ra[j] >> 16;
+        int iy = (oy == 0x7fff) ? -1 : oy * sstride + dy;
+        int ix = rx[j] * sstride + dx;
+        const bool in = (c < cin) & ((unsigned)iy < lh) & ((unsigned)ix < lw);
+        iy >>= sup;
+        ix >>= sup;
+        const bool second = c >= csplit;
+        const unsigned ld = second ? ld1 : ld0;
+        const unsigned cc = second ? c - csplit : c;
+        const half_t* base = second ? src1 : src0;
+        const unsigned pix = ((unsigned)(bimg * sh + iy)) * (unsigned)sw + (unsigned)ix;
+        const unsigned off = pix * ld + cc;
+        src = in ? base + off : zero;
+      } else {
+        src = p.W + (size_t)ra[j] * p.ldw + kcol + rchunk * 8;
+      }
+      __builtin_amdgcn_global_load_lds((const void*)src, dst, 16, 0, 0);
+    }
+  };
+
+  f16v acc[CF::FM][CF::FN];
+#pragma unroll
+  for (int i = 0; i < CF::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < CF::FN; ++j) acc[i][j] = f16v{};
+
+  const int fr = lane & 31, fh = lane >> 5;
+  const int arow0 = wm * CF::TM + fr;
+  const int brow0 = CF::TBM + wn * CF::TN + fr;
+  if (kt0 < kt1) stage(kt0, 0);
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int cur = (kt - kt0) & 1;
+    if (kt + 1 < kt1) {
+      stage(kt + 1, cur ^ 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPW) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    const half_t* st = lds + cur * CF::STAGE_H;
+#pragma unroll
+    for (int kk = 0; kk < BK / 16; ++kk) {
+      h8 fa[CF::FM], fb[CF::FN];
+#pragma unroll
+      for (int i = 0; i < CF::FM; ++i)
+        fa[i] = *reinterpret_cast<const h8*>(st + swz(arow0 + i * 32, kk * 2 + fh));
+#pragma unroll
+      for (int j = 0; j < CF::FN; ++j)
+        fb[j] = *reinterpret_cast<const h8*>(st + swz(brow0 + j * 32, kk * 2 + fh));
+#pragma unroll
+      for (int i = 0; i < CF::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < CF::FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();      // everyone done reading `cur` before it is restaged
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  epilogue_direct<CF::FM, CF::FN>(p, acc, m0, n0, wm * CF::TM, wn * CF::TN, blockIdx.y);
+}
+
+using Cfg256x256 = Cfg<256, 256, 2, 4>;
+using Cfg256x128 = Cfg<256, 128, 4, 2>;
+using Cfg128x128 = Cfg<128, 128, 2, 2>;
+// N = 320 / 640 / 960 levels of SD: 32x160 wave tiles (5 MFMA tiles per wave)
+using Cfg256x320 = Cfg<256, 320, 8, 2>;   // 16 waves
+using Cfg256x160 = Cfg<256, 160, 8, 1>;
+using Cfg128x320 = Cfg<128, 320, 4, 2>;
 
 // Split-K reduction + epilogue: 8 columns per thread.
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(Params p) {
@@ -401,6 +690,19 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(Params p) {
   }
 }
 
+template <class CF>
+int launch_glds(const Params& p, dim3 grid, hipStream_t s) {
+  static bool attr_set = false;   // raise the dynamic-LDS cap once per instantiation (not a per-call alloc)
+  if (!attr_set) {
+    if (hipFuncSetAttribute((const void*)conv_glds_kernel<CF>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            CF::LDS_BYTES) != hipSuccess)
+      return fail(SDK_EHIP, "conv2d: cannot raise the dynamic LDS limit");
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(conv_glds_kernel<CF>, grid, dim3(CF::NT), CF::LDS_BYTES, s, p);
+  return check_launch("conv_glds");
+}
+
 int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   if (!a) return fail(SDK_EINVAL, "conv2d: null args");
   if (a->nseg < 1 || a->nseg > 2) return fail(SDK_EINVAL, "conv2d: nseg must be 1 or 2");
@@ -411,7 +713,6 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   p.batch = a->batch; p.ho = a->ho; p.wo = a->wo; p.hw_out = a->ho * a->wo;
   p.M = a->batch * p.hw_out;
   p.N = a->cout;
-  p.Npad = (a->cout + BN - 1) / BN * BN;
   p.nseg = a->nseg;
   double kreal = 0;
   int kt = 0, koff = 0;
@@ -446,17 +747,84 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   }
   if (a->out_mode == SDK_OUT_GEGLU_F16 && (a->cout % 64)) return fail(SDK_EINVAL, "conv2d: GEGLU cout % 64");
   p.kt_total = kt;
-  p.W = (const half_t*)a->weight; p.ldw = a->k_total;
+  p.W = (const half_t*)a->weight; p.ldw = a->k_total; p.wrows = (a->cout + 127) / 128 * 128;
   p.bias = a->bias; p.row_bias = a->row_bias; p.rb_ld = a->row_bias_ld;
   p.res = (const half_t*)a->residual; p.res_ld = a->res_ld;
   p.out = a->out; p.out_ld = a->out_ld; p.out_mode = a->out_mode;
-  p.tiles_m = (p.M + BM - 1) / BM; p.tiles_n = p.Npad / BN;
+  bool transform = false;
+  for (int s = 0; s < a->nseg; ++s) {
+    const sdk_conv_src& g = a->seg[s];
+    transform |= (g.gn_scale != nullptr) || g.silu;
+    // the LDS-DMA kernels address sources with 32-bit element offsets
+    if ((double)a->batch * g.h * g.w * std::max(g.ld0, g.ld1) >= 4294967296.0) transform = true;
+  }
+  // tile configuration: LDS-DMA kernels for transform-free operands, scored by
+  // padded-work efficiency x whole-chip wave quantisation x measured per-config
+  // throughput
+  struct Opt { int variant, bm, bn, nw; double pref; bool geglu_ok; };
+  // relative throughput of each config on shapes it tiles exactly (tools/bench_conv.py, MI355X)
+  const Opt opts[] = {{2, 256, 256, 8, 1.00, true}, {5, 256, 320, 16, 0.92, false},
+                      {7, 128, 320, 8, 0.88, false}, {6, 256, 160, 8, 0.72, false},
+                      {4, 128, 128, 4, 0.72, true}, {3, 256, 128, 8, 0.65, true}};
+  int var = 0, tbm = BM, tbn = BN, best_split = 0;
+  auto pick_split = [&](int tiles, int slots, double& fill) {
+    int best = 1;
+    double bf = -1;
+    for (int sp = 1; sp <= 16; sp *= 2) {
+      if (sp > 1 && kt / sp < 8) break;
+      const int blocks = tiles * sp;
+      const double waves = (double)((blocks + slots - 1) / slots);
+      double f = (double)blocks / (waves * slots);
+      for (int q = 1; q < sp; q *= 2) f *= 0.95;      // slab write + reduce traffic
+      if (f > bf + 1e-9) { bf = f; best = sp; }
+    }
+    fill = bf;
+    return best;
+  };
+  if (!transform) {
+    double best = -1;
+    for (const Opt& o : opts) {
+      if (a->out_mode == SDK_OUT_GEGLU_F16 && !o.geglu_ok) continue;
+      const int tmm = (p.M + o.bm - 1) / o.bm, tnn = (p.N + o.bn - 1) / o.bn;
+      const double eff = (double)p.M * p.N / ((double)tmm * o.bm * tnn * o.bn);
+      double fill;
+      const bool can_split = a->out_mode != SDK_OUT_GEGLU_F16 && a->cout % 8 == 0;
+      const int per = (o.variant == 4) ? 2 : 1;
+      const int sp = can_split ? pick_split(tmm * tnn, 256 * per, fill) : 1;
+      if (!can_split) {
+        const int slots = 256 * per, blocks = tmm * tnn;
+        fill = (double)blocks / ((double)((blocks + slots - 1) / slots) * slots);
+      }
+      const double score = eff * fill * o.pref;
+      if (score > best) { best = score; var = o.variant; tbm = o.bm; tbn = o.bn; best_split = sp; }
+    }
+  }
+  // tuning override (benchmarks only): SDK_CONV_VARIANT=0|2|3|4|5
+  const char* fe = getenv("SDK_CONV_VARIANT");
+  const int forced = fe ? atoi(fe) : -1;
+  if (forced >= 0 && forced <= 7 && forced != 1 && (forced == 0 || !transform) &&
+      !(forced >= 5 && a->out_mode == SDK_OUT_GEGLU_F16)) {
+    static const int fbm[8] = {128, 0, 256, 256, 128, 256, 256, 128};
+    static const int fbn[8] = {128, 0, 256, 128, 128, 320, 160, 320};
+    var = forced;
+    tbm = fbm[forced];
+    tbn = fbn[forced];
+    best_split = 0;
+  }
+  p.variant = var;
+  p.tiles_m = (p.M + tbm - 1) / tbm;
+  p.tiles_n = (p.N + tbn - 1) / tbn;
+  p.Npad = p.tiles_n * tbn;                       // split-K slab row stride
   const int tiles = p.tiles_m * p.tiles_n;
+  const int per_cu = (var == 0 || var == 4) ? 2 : 1;
   int split = a->split_k;
   if (split <= 0) {
-    split = 1;
-    // fill the 256 CUs x 2 resident workgroups; keep >= 8 K tiles per split
-    while (tiles * split < 384 && kt / (split * 2) >= 8 && split < 16) split *= 2;
+    if (best_split > 0) {
+      split = best_split;
+    } else {
+      split = 1;
+      while (tiles * split < 256 * per_cu && kt / (split * 2) >= 8 && split < 16) split *= 2;
+    }
   }
   if (a->out_mode == SDK_OUT_GEGLU_F16 || a->cout % 8) split = 1;
   if (split > kt) split = kt;
@@ -468,7 +836,7 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
     info->split_k = split;
     info->grid_tiles = tiles;
     info->workspace_bytes = ws;
-    info->variant = split > 1 ? 1 : 0;
+    info->variant = var;
     info->flops = 2.0 * p.M * (double)p.N * kreal;
   }
   if (split > 1) {
@@ -497,8 +865,18 @@ extern "C" int sdk_conv2d(const sdk_conv_args* a, sdk_stream_t stream) {
     return fail(SDK_EWORKSPACE, "conv2d: split-K workspace too small");
   hipStream_t s = (hipStream_t)stream;
   dim3 grid(p.tiles_m * p.tiles_n, p.split);
-  hipLaunchKernelGGL(conv_igemm_kernel, grid, dim3(NT), 0, s, p);
-  if (int e = check_launch("conv_igemm")) return e;
+  switch (p.variant) {
+    case 2: rc = launch_glds<Cfg256x256>(p, grid, s); break;
+    case 3: rc = launch_glds<Cfg256x128>(p, grid, s); break;
+    case 4: rc = launch_glds<Cfg128x128>(p, grid, s); break;
+    case 5: rc = launch_glds<Cfg256x320>(p, grid, s); break;
+    case 6: rc = launch_glds<Cfg256x160>(p, grid, s); break;
+    case 7: rc = launch_glds<Cfg128x320>(p, grid, s); break;
+    default:
+      hipLaunchKernelGGL(conv_igemm_kernel, grid, dim3(NT), 0, s, p);
+      rc = check_launch("conv_igemm");
+  }
+  if (rc) return rc;
   if (p.split > 1) {
     const size_t total = (size_t)p.M * (p.N / 8);
     int blocks = (int)std::min<size_t>((total + 255) / 256, 4096);

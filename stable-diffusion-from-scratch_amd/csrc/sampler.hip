@@ -163,7 +163,12 @@ extern "C" int sdk_version(void) { return 1; }
 extern "C" const char* sdk_kernel_name(int32_t variant) {
   switch (variant) {
     case 0: return "conv_igemm_kernel";
-    case 1: return "conv_igemm_kernel+splitk_reduce_kernel";
+    case 2: return "conv_glds_kernel<Cfg<256,256,2,4>>";
+    case 3: return "conv_glds_kernel<Cfg<256,128,4,2>>";
+    case 4: return "conv_glds_kernel<Cfg<128,128,2,2>>";
+    case 5: return "conv_glds_kernel<Cfg<256,320,8,2>>";
+    case 6: return "conv_glds_kernel<Cfg<256,160,8,1>>";
+    case 7: return "conv_glds_kernel<Cfg<128,320,4,2>>";
     default: return "unknown";
   }
 }

@@ -19,7 +19,7 @@ from ._lib import (AttentionArgs, ConvArgs, ConvPlanInfo, DdimArgs, GroupNormArg
                    OUT_NHWC_F16, OUT_ROWS_F32, check, lib)
 
 BK = 64          # K tile of the conv kernel (packed weight column padding)
-BN = 128         # N tile (packed weight row padding)
+BN = 128         # packed weight row padding (the kernels clamp reads beyond it)
 
 
 def _stream():

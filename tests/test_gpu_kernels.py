@@ -42,6 +42,20 @@ def _conv_ref(x_nhwc, w, b, stride=1, pad=1, upsample=False, gn=None, silu=False
     return F.conv2d(x, w.float(), None if b is None else b.float(), stride=stride, padding=pad).permute(0, 2, 3, 1)
 
 
+@pytest.fixture(params=["auto", "0", "2", "3", "4", "5", "6", "7"])
+def conv_variant(request):
+    """Every conv kernel variant (register-staged 128x128, LDS-DMA 256x256/256x128/128x128)."""
+    import os
+    old = os.environ.get("SDK_CONV_VARIANT")
+    if request.param != "auto":
+        os.environ["SDK_CONV_VARIANT"] = request.param
+    yield request.param
+    if old is None:
+        os.environ.pop("SDK_CONV_VARIANT", None)
+    else:
+        os.environ["SDK_CONV_VARIANT"] = old
+
+
 @pytest.mark.parametrize("B,H,W,Cin,Cout,k,stride,up", [
     (2, 16, 16, 64, 128, 3, 1, False),
     (2, 16, 16, 320, 320, 3, 1, False),
@@ -51,7 +65,7 @@ def _conv_ref(x_nhwc, w, b, stride=1, pad=1, upsample=False, gn=None, silu=False
     (3, 10, 6, 96, 40, 1, 1, False),          # ragged M, N not a multiple of 128
     (2, 8, 8, 8, 320, 3, 1, False),           # conv_in (8 padded channels)
 ])
-def test_conv(ops, B, H, W, Cin, Cout, k, stride, up):
+def test_conv(ops, conv_variant, B, H, W, Cin, Cout, k, stride, up):
     x = _rand(B, H, W, Cin, seed=1)
     w = torch.randn(Cout, Cin, k, k) / math.sqrt(Cin * k * k)
     b = torch.randn(Cout) * 0.1
@@ -62,7 +76,7 @@ def test_conv(ops, B, H, W, Cin, Cout, k, stride, up):
     assert rel_l2(y, ref) < 2e-3
 
 
-def test_conv_gn_silu_concat_fused_skip_rowbias(ops):
+def test_conv_gn_silu_concat_fused_skip_rowbias(ops, conv_variant):
     """ResBlock conv2 shape: GN+SiLU prologue over a 2-source concat is tested via conv1,
     the fused 1x1 shortcut segment and the per-(batch, channel) embedding add via conv2."""
     B, H, W, C1, C2, Co = 2, 8, 8, 64, 32, 64
@@ -91,7 +105,7 @@ def test_conv_gn_silu_concat_fused_skip_rowbias(ops):
     assert rel_l2(y2, ref2) < 3e-3
 
 
-def test_linear_residual_geglu_rows_f32(ops):
+def test_linear_residual_geglu_rows_f32(ops, conv_variant):
     M, K, N = 300, 320, 640
     x = _rand(M, K, seed=4)
     w = torch.randn(N, K) / math.sqrt(K)
@@ -117,7 +131,7 @@ def test_linear_residual_geglu_rows_f32(ops):
     assert y32.dtype == torch.float32 and rel_l2(y32, ref32) < 2e-3
 
 
-def test_conv_nchw_f32_out(ops):
+def test_conv_nchw_f32_out(ops, conv_variant):
     B, H, W, Cin, Cout = 2, 16, 16, 64, 4
     x = _rand(B, H, W, Cin, seed=6)
     w = torch.randn(Cout, Cin, 3, 3) / math.sqrt(Cin * 9)
