@@ -145,6 +145,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-autotune", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -189,8 +190,11 @@ def main():
             tdist.barrier()
         torch.cuda.synchronize()
 
+    # the first warm-up step also autotunes every distinct conv problem (tile config x split-K)
+    ops.AUTOTUNE.enable(not args.no_autotune)
     for _ in range(args.warmup):
         one_step()
+    ops.AUTOTUNE.enable(False)
     barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -229,7 +233,8 @@ def main():
            "config": {"workload": cfg["workload"], "global_batch": world * B, "batch_per_gpu": B,
                       "latent": [4, L, L], "image": [3, 8 * L, 8 * L], "ddim_steps": args.ddim_steps, "eta": 0.0,
                       "parallelism": f"dp{world}", "collective": "all_gather decoded images (RCCL)" if dist else None},
-           "unet_step_ms": round(unet_ms, 3), "finite": finite}
+           "unet_step_ms": round(unet_ms, 3), "finite": finite,
+           "autotuned_conv_problems": len(ops.AUTOTUNE.table)}
     if not args.no_roofline and rank == 0:
         summ = ops.PROFILER.summary()
         conv = {"launches": 0, "ms": 0.0, "flops": 0.0}
@@ -246,6 +251,10 @@ def main():
                                "launches": conv["launches"], "avg_launch_us": round(1e6 * avg_s, 2),
                                "flops_per_launch": conv["flops"] / conv["launches"]}
         out["kernel_time_ms_last_step"] = {k: round(v["ms"], 2) for k, v in summ.items()}
+        if os.environ.get("BENCH_SHAPES_OUT"):
+            with open(os.environ["BENCH_SHAPES_OUT"], "w") as f:
+                for (kind, shape), n, ms, tf in ops.PROFILER.shape_table():
+                    f.write(f"{kind:10s} {str(shape):44s} launches={n:5d} ms={ms:9.2f} TFLOP/s={tf:7.1f}\n")
         tot_tf = (unet_gflops_per_image(args.config) * args.ddim_steps + vae_gflops_per_image(args.config)) / 1000
         out["end_to_end_tflops"] = round(tot_tf * value, 1)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -93,6 +93,7 @@ typedef struct {
   int32_t split_k;         /* 0 = choose; 1 = off */
   float* workspace;        /* split-K fp32 partials */
   int64_t workspace_bytes;
+  int32_t variant_hint;    /* 0 = choose; 1 + variant id forces a tile configuration (autotuning) */
 } sdk_conv_args;
 
 typedef struct {

@@ -27,7 +27,7 @@ class ConvArgs(C.Structure):
     _fields_ = [("batch", i32), ("ho", i32), ("wo", i32), ("cout", i32), ("nseg", i32), ("seg", ConvSrc * 2),
                 ("weight", vp), ("k_total", i32), ("bias", vp), ("row_bias", vp), ("row_bias_ld", i32),
                 ("residual", vp), ("res_ld", i32), ("out", vp), ("out_ld", i32), ("out_mode", i32),
-                ("split_k", i32), ("workspace", vp), ("workspace_bytes", i64)]
+                ("split_k", i32), ("workspace", vp), ("workspace_bytes", i64), ("variant_hint", i32)]
 
 
 class ConvPlanInfo(C.Structure):

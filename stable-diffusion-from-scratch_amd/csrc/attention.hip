@@ -6,12 +6,19 @@
 // transposed, S^T = K Q^T (A = K rows from LDS, B = Q^T fragments held in
 // registers for the whole loop), so each lane owns ONE query row: the softmax
 // row max / row sum are in-register reductions plus one exchange with lane^32.
-// The S^T accumulator is then, converted to fp16, directly the B operand of
-// O^T += V^T P^T (the accumulator's row index = the key = the contraction
-// index), with the V^T operand read from a transposed LDS image whose rows are
-// padded to 136 B so the ds_read_b64 fragment reads are bank-conflict-free.
-// Head dims that are not multiples of 16/32 (40, 80, 160 in SD-1) are
-// zero-padded inside LDS/registers only; HBM traffic is the unpadded tensors.
+// The S^T accumulator, converted to fp16, is directly the B operand of
+// O^T += V^T P^T (its row index = the key = the contraction index).  V stays
+// row-major in LDS and the V^T operand is read with ds_read_b64_tr_b16 (the
+// hardware transpose read), rows padded so a 32-lane half touches 64 distinct
+// banks.
+//
+// Per-tile VALU is the budget at small head dims (d = 40: 14 MFMAs per 64-key
+// tile), so: the softmax scale is one FMA feeding v_exp_f32 (scores stay raw),
+// key masking runs only in a ragged last tile, the O rescale is skipped when
+// no lane's running max grew, and when d is below the padded V width the row
+// sum comes out of the PV MFMA itself (a ones column in V's zero padding).
+// Head dims that are not multiples of 16/32 (40, 80, 160 in SD-1) are padded
+// inside LDS/registers only; HBM traffic is the unpadded tensors.
 #include "common.h"
 
 namespace sdk {
@@ -24,17 +31,22 @@ struct AttnParams {
   half_t* o;
   int q_ld, k_ld, v_ld, o_ld;
   int batch, heads, nq, nk, d;
-  float scale_log2;
+  float c;              // scale * log2(e)
 };
 
+typedef __fp16 fp16x4_t __attribute__((ext_vector_type(4)));
+
 constexpr int KT = 64;          // keys per tile
-constexpr int VLD = KT + 4;     // V^T row stride (halfs): 136 B
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 template <int DQK, int DV>
 __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnParams p) {
-  constexpr int KLD = DQK + 8;
-  __shared__ __attribute__((aligned(16))) half_t Ks[KT * KLD];
-  __shared__ __attribute__((aligned(16))) half_t Vt[DV * VLD];
+  constexpr int KLD = DQK + 8;                                       // K row stride (halfs)
+  constexpr int VLD = ((DV * 2 / 64) % 2 == 0) ? DV + 32 : DV;       // V row stride: 64 or 192 B mod 256
+  __shared__ __attribute__((aligned(16))) half_t smem[KT * KLD + KT * VLD];
+  half_t* Ks = smem;
+  half_t* Vs = smem + KT * KLD;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 31, fh = lane >> 5;
@@ -42,6 +54,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnParams p) {
   const int q0 = blockIdx.x * 128 + wave * 32;
   const int qrow = q0 + fr;
   const bool qvalid = qrow < p.nq;
+  const bool ones_row = p.d < DV;          // row sum from the PV MFMA (ones column at d)
 
   // Q^T fragments (B operand): lane holds Q[qrow][ks*16 + 8*fh + j]
   h8 qf[DQK / 16];
@@ -65,10 +78,16 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnParams p) {
   const half_t* vbase = p.v + (size_t)b * p.nk * p.v_ld + head * p.d;
   const int ntiles = (p.nk + KT - 1) / KT;
 
+  // transposed-read addressing for the V^T operand (32x32x16, A side):
+  // group g = lane>>4 reads keys 16ks + 4*(g>>1) + 8*hi .. +3, columns 32*db + 16*(g&1) .. +15;
+  // lane 4q+pp of the group supplies row q, columns 4pp..4pp+3
+  const int g = lane >> 4, q4 = (lane & 15) >> 2, pp = lane & 3;
+  const int vrow_off = 4 * (g >> 1) + q4;
+  const int vcol_off = 16 * (g & 1) + 4 * pp;
+
   for (int t = 0; t < ntiles; ++t) {
     const int key0 = t * KT;
     __syncthreads();   // previous tile fully consumed
-    // K tile: [64 keys][DQK] (coalesced 16-B chunks along d)
     for (int e = tid; e < KT * (DQK / 8); e += 256) {
       const int kr = e / (DQK / 8), c = e - kr * (DQK / 8);
       const int key = key0 + kr, dd = c * 8;
@@ -76,18 +95,22 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnParams p) {
       if (key < p.nk && dd < p.d) v = *reinterpret_cast<const h8*>(kbase + (size_t)key * p.k_ld + dd);
       *reinterpret_cast<h8*>(Ks + kr * KLD + dd) = v;
     }
-    // V^T tile: [DV][64 keys]
     for (int e = tid; e < KT * (DV / 8); e += 256) {
       const int kr = e / (DV / 8), c = e - kr * (DV / 8);
       const int key = key0 + kr, dd = c * 8;
       h8 v = {};
-      if (key < p.nk && dd < p.d) v = *reinterpret_cast<const h8*>(vbase + (size_t)key * p.v_ld + dd);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) Vt[(dd + j) * VLD + kr] = v[j];
+      if (key < p.nk) {
+        if (dd + 8 <= p.d) {
+          v = *reinterpret_cast<const h8*>(vbase + (size_t)key * p.v_ld + dd);
+        } else if (ones_row && dd <= p.d && p.d < dd + 8) {
+          v[p.d - dd] = (half_t)1.0f;       // ones column -> row sum of P in O^T row d
+        }
+      }
+      *reinterpret_cast<h8*>(Vs + kr * VLD + dd) = v;
     }
     __syncthreads();
 
-    // S^T = K Q^T for two 32-key sub-blocks
+    // S^T = K Q^T for two 32-key sub-blocks (raw, unscaled scores)
     f16v s[2];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
@@ -98,24 +121,34 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnParams p) {
         s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, qf[ks], s[kb], 0, 0, 0);
       }
     }
-    // scale, mask, row max (keys are rows: regs + lane^32)
-    float mt = -1e30f;
+    if (key0 + KT > p.nk) {           // ragged last tile only
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+          if (key >= p.nk) s[kb][r] = -1e30f;
+        }
+    }
+    float mt = s[0][0];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
-        float x = s[kb][r] * p.scale_log2;
-        if (key >= p.nk) x = -1e30f;
-        s[kb][r] = x;
-        mt = fmaxf(mt, x);
-      }
+      for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[kb][r]);
     mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
     const float m_new = fmaxf(m_run, mt);
-    const float alpha = exp2f(m_run - m_new);
-    m_run = m_new;
-    float ls = 0.f;
+    if (__any(m_new > m_run)) {       // rescale only when some row's max grew
+      const float alpha = fast_exp2((m_run - m_new) * p.c);
+      l_run *= alpha;
+#pragma unroll
+      for (int db = 0; db < DV / 32; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[db][r] *= alpha;
+      m_run = m_new;
+    }
+    const float nmc = -m_run * p.c;
     h8 pf[4];
+    float ls = 0.f;
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
@@ -123,48 +156,55 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnParams p) {
         h8 pk;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float e = exp2f(s[kb][hlf * 8 + j] - m_new);
-          ls += e;
+          const float e = fast_exp2(fmaf(s[kb][hlf * 8 + j], p.c, nmc));
+          if (!ones_row) ls += e;
           pk[j] = (half_t)e;
         }
         pf[kb * 2 + hlf] = pk;
       }
-    ls += __shfl_xor(ls, 32, 64);
-    l_run = l_run * alpha + ls;
-#pragma unroll
-    for (int db = 0; db < DV / 32; ++db)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) o[db][r] *= alpha;
+    if (!ones_row) l_run += ls + __shfl_xor(ls, 32, 64);
 
-    // O^T += V^T P^T ; k-step ks covers keys 16ks..16ks+15, element j of lane half fh is
-    // key 16ks + 8(j>>2) + 4fh + (j&3) (accumulator row order)
+    // O^T += V^T P^T ; element j of lane half fh in k-step ks is key 16ks + 8(j>>2) + 4fh + (j&3)
 #pragma unroll
     for (int db = 0; db < DV / 32; ++db) {
-      const half_t* vr = Vt + (db * 32 + fr) * VLD + 4 * fh;
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        const h4 lo = *reinterpret_cast<const h4*>(vr + ks * 16);
-        const h4 hi = *reinterpret_cast<const h4*>(vr + ks * 16 + 8);
-        h8 a;
-        a[0] = lo[0]; a[1] = lo[1]; a[2] = lo[2]; a[3] = lo[3];
-        a[4] = hi[0]; a[5] = hi[1]; a[6] = hi[2]; a[7] = hi[3];
+        const half_t* base = Vs + (16 * ks + vrow_off) * VLD + 32 * db + vcol_off;
+        const fp16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4f16(
+            (__attribute__((address_space(3))) fp16x4_t*)(base));
+        const fp16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4f16(
+            (__attribute__((address_space(3))) fp16x4_t*)(base + 8 * VLD));
+        const h4 lo4 = __builtin_bit_cast(h4, lo), hi4 = __builtin_bit_cast(h4, hi);
+        const h8 a = __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7);
         o[db] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, pf[ks], o[db], 0, 0, 0);
       }
     }
   }
 
+  // row sum: explicit, or O^T row d (block d/32, row rho = d%32 held by lanes with h = (rho>>2)&1)
+  float l = l_run;
+  if (ones_row) {
+    const int rho = p.d & 31, hsrc = (rho >> 2) & 1, rsel = (rho & 3) + 4 * (rho >> 3);
+    float v = 0.f;
+#pragma unroll
+    for (int db = 0; db < DV / 32; ++db)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (db == (p.d >> 5) && r == rsel) v = o[db][r];
+    l = __shfl(v, fr + 32 * hsrc, 64);
+  }
   if (!qvalid) return;
-  const float inv = 1.f / l_run;
+  const float inv = 1.f / l;
   half_t* op = p.o + ((size_t)b * p.nq + qrow) * p.o_ld + head * p.d;
 #pragma unroll
   for (int db = 0; db < DV / 32; ++db)
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int dd = db * 32 + 8 * g + 4 * fh;
+    for (int gg = 0; gg < 4; ++gg) {
+      const int dd = db * 32 + 8 * gg + 4 * fh;
       if (dd < p.d) {
         h4 w;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) w[j] = (half_t)(o[db][4 * g + j] * inv);
+        for (int j = 0; j < 4; ++j) w[j] = (half_t)(o[db][4 * gg + j] * inv);
         *reinterpret_cast<h4*>(op + dd) = w;
       }
     }

@@ -799,9 +799,10 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
       if (score > best) { best = score; var = o.variant; tbm = o.bm; tbn = o.bn; best_split = sp; }
     }
   }
-  // tuning override (benchmarks only): SDK_CONV_VARIANT=0|2|3|4|5
+  // forced configuration: the caller's autotuner (variant_hint = 1 + id) or, for
+  // benchmarks, SDK_CONV_VARIANT=id
   const char* fe = getenv("SDK_CONV_VARIANT");
-  const int forced = fe ? atoi(fe) : -1;
+  const int forced = a->variant_hint > 0 ? a->variant_hint - 1 : (fe ? atoi(fe) : -1);
   if (forced >= 0 && forced <= 7 && forced != 1 && (forced == 0 || !transform) &&
       !(forced >= 5 && a->out_mode == SDK_OUT_GEGLU_F16)) {
     static const int fbm[8] = {128, 0, 256, 256, 128, 256, 256, 128};

@@ -157,6 +157,66 @@ class PackedConv:
         self.bias = b.to(device=device, dtype=torch.float32).contiguous() if b is not None else None
 
 
+class _Autotune:
+    """Per-shape choice of conv tile configuration and split-K, measured on the device.
+
+    Enabled by ``enable()`` (UNetModel/AutoEncoderKL.prepare(autotune=True)); the
+    first call of each distinct problem times every candidate (HIP events, 3 reps
+    after a warm-up) and caches the fastest.  Never runs under graph capture."""
+    VARIANTS = (2, 5, 7, 6, 4, 3)
+    SPLITS = (0, 1, 2, 4, 8)
+
+    def __init__(self):
+        self.enabled = False
+        self.table = {}
+
+    def enable(self, on=True):
+        self.enabled = on
+
+    def key(self, a, pc):
+        s0, s1 = a.seg[0], a.seg[1]
+        return (a.batch, a.ho, a.wo, a.cout, a.nseg, pc.k_total, a.out_mode, s0.cin, s0.h, s0.w, s0.ksize,
+                s0.stride, s0.upsample, s0.c_split, bool(s0.gn_scale) or bool(s0.silu), s1.cin if a.nseg > 1 else 0)
+
+    def choose(self, a, pc, dev):
+        key = self.key(a, pc)
+        hit = self.table.get(key)
+        if hit is not None or not self.enabled or torch.cuda.is_current_stream_capturing():
+            return hit
+        if a.seg[0].gn_scale or a.seg[0].silu or (a.nseg > 1 and (a.seg[1].gn_scale or a.seg[1].silu)):
+            self.table[key] = (0, 0)
+            return self.table[key]
+        best, best_t = (0, 0), float("inf")
+        info = ConvPlanInfo()
+        stream = _stream()
+        for v in self.VARIANTS:
+            for sp in self.SPLITS:
+                a.variant_hint, a.split_k = v + 1, sp
+                if lib().sdk_conv2d_plan(C.byref(a), C.byref(info)) != 0:
+                    continue
+                if sp == 0 and info.split_k in self.SPLITS[1:]:
+                    continue             # the automatic split equals an explicit candidate
+                if info.workspace_bytes > 0:
+                    ws = WORKSPACE.get(info.workspace_bytes, dev)
+                    a.workspace, a.workspace_bytes = ws.data_ptr(), ws.numel()
+                check(lib().sdk_conv2d(C.byref(a), stream), "conv2d(autotune)")
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(3):
+                    lib().sdk_conv2d(C.byref(a), stream)
+                e1.record()
+                e1.synchronize()
+                t = e0.elapsed_time(e1)
+                if t < best_t:
+                    best_t, best = t, (v + 1, info.split_k)
+        a.variant_hint, a.split_k = 0, 0
+        self.table[key] = best
+        return best
+
+
+AUTOTUNE = _Autotune()
+
+
 def conv2d(pc: PackedConv, x, *, ksize=None, stride=1, pad=None, upsample=False, gn=None, silu=False,
            seg2=None, bias=True, row_bias=None, residual=None, out_mode=OUT_NHWC_F16, out=None):
     """Run the implicit-GEMM conv.  ``seg2`` = (x2, gn2, silu2) adds a fused 1x1 K segment.
@@ -199,6 +259,9 @@ def conv2d(pc: PackedConv, x, *, ksize=None, stride=1, pad=None, upsample=False,
         _need_cuda(residual, "conv2d residual")
         a.residual = residual.data_ptr()
         a.res_ld = residual.shape[-1]
+    tuned = AUTOTUNE.choose(a, pc, dev) if (AUTOTUNE.enabled or AUTOTUNE.table) else None
+    if tuned is not None:
+        a.variant_hint, a.split_k = tuned
     info = ConvPlanInfo()
     check(lib().sdk_conv2d_plan(C.byref(a), C.byref(info)), "conv2d_plan")
     if info.workspace_bytes > 0:
@@ -206,7 +269,7 @@ def conv2d(pc: PackedConv, x, *, ksize=None, stride=1, pad=None, upsample=False,
         a.workspace = ws.data_ptr()
         a.workspace_bytes = ws.numel()
     if PROFILER.active:
-        PROFILER.begin("conv", info)
+        PROFILER.begin("conv", info, shape=(B * Ho * Wo, pc.N, pc.k_total, info.variant, info.split_k))
     check(lib().sdk_conv2d(C.byref(a), _stream()), "conv2d")
     if PROFILER.active:
         PROFILER.end()
@@ -398,7 +461,7 @@ class _Profiler:
     def stop(self):
         self.active = False
 
-    def begin(self, kind, info):
+    def begin(self, kind, info, shape=None):
         s = torch.cuda.current_stream()
         e0 = torch.cuda.Event(enable_timing=True)
         e0.record(s)
@@ -406,20 +469,33 @@ class _Profiler:
         if kind == "attention" and info is not None:
             b, h, nq, nk, d = info
             flops = 4.0 * b * h * nq * nk * d
+            shape = info
         variant = info.variant if isinstance(info, ConvPlanInfo) else None
-        self._cur = (kind, variant, flops, e0)
+        self._cur = (kind, variant, flops, e0, shape)
 
     def end(self):
         s = torch.cuda.current_stream()
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record(s)
-        kind, variant, flops, e0 = self._cur
-        self.records.append((kind, variant, flops, e0, e1))
+        kind, variant, flops, e0, shape = self._cur
+        self.records.append((kind, variant, flops, e0, e1, shape))
+
+    def shape_table(self):
+        """Per (kind, shape) totals: launches, ms, TFLOP/s — where the time goes."""
+        torch.cuda.synchronize()
+        out = {}
+        for kind, variant, flops, e0, e1, shape in self.records:
+            d = out.setdefault((kind, shape), [0, 0.0, 0.0])
+            d[0] += 1
+            d[1] += e0.elapsed_time(e1)
+            d[2] += flops or 0.0
+        rows = [(k, v[0], v[1], (v[2] / (v[1] * 1e-3) / 1e12) if v[1] > 0 and v[2] else 0.0) for k, v in out.items()]
+        return sorted(rows, key=lambda r: -r[2])
 
     def summary(self):
         torch.cuda.synchronize()
         out = {}
-        for kind, variant, flops, e0, e1 in self.records:
+        for kind, variant, flops, e0, e1, shape in self.records:
             key = kind if variant is None else f"{kind}:{variant}"
             d = out.setdefault(key, {"launches": 0, "ms": 0.0, "flops": 0.0})
             d["launches"] += 1
