@@ -498,6 +498,132 @@ struct Cfg {
   static_assert(LDS_BYTES <= 160 * 1024, "two stages must fit the 160 KiB LDS");
 };
 
+#define SDK_SEGF(f) (s1 ? p.seg[1].f : p.seg[0].f)
+
+// The DMA goes through buffer resources: 32-bit byte offsets and the hardware range
+// check — an offset past num_records loads zeros, which is the conv's zero padding and
+// the ragged tile edge, with no per-lane pointer select.
+constexpr unsigned PH_OOB = 0x80000000u;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ph_rsrc(const void* base, long long bytes) {
+  const int n = (int)(bytes < 0x7fffffffLL ? bytes : 0x7fffffffLL);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, n, 0x00020000);
+}
+
+__device__ __forceinline__ void ph_dma(__amdgpu_buffer_rsrc_t r, half_t* dst, unsigned voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)dst, 16, voff, soff, 0, 0);
+}
+
+// K-step -> (segment, tap row, tap column, channel base); scalar.
+__device__ __forceinline__ void ph_kstate(const Params& p, int kt, int& seg, int& ky, int& kx, int& cb) {
+  const bool s1 = p.nseg > 1 && kt >= p.seg[1].kt_begin;
+  seg = s1 ? 1 : 0;
+  const int local = kt - SDK_SEGF(kt_begin), tpt = SDK_SEGF(tiles_per_tap), ks = SDK_SEGF(ksize);
+  const int tap = local / tpt;
+  cb = (local - tap * tpt) * BK;
+  ky = tap / ks;
+  kx = tap - ky * ks;
+}
+
+__device__ __forceinline__ void ph_kadv(const Params& p, int& seg, int& ky, int& kx, int& cb) {
+  const bool s1 = seg != 0;
+  cb += BK;
+  if (cb >= SDK_SEGF(cin_pad)) {
+    cb = 0;
+    const int ks = SDK_SEGF(ksize);
+    if (++kx == ks) {
+      kx = 0;
+      if (++ky == ks) { ky = 0; ++seg; }
+    }
+  }
+}
+
+struct DmaSrc {
+  __amdgpu_buffer_rsrc_t a0, a1, s0, s1, w;
+};
+
+__device__ __forceinline__ DmaSrc make_dma_src(const Params& p) {
+  const Seg& g0 = p.seg[0];
+  const Seg& g1 = p.seg[1];
+  const long long npix0 = (long long)p.batch * g0.h * g0.w;
+  const bool two = p.nseg > 1;
+  DmaSrc d;
+  d.a0 = ph_rsrc(g0.src0, npix0 * g0.ld0 * 2);
+  d.a1 = ph_rsrc(g0.src1 ? g0.src1 : g0.src0, npix0 * (g0.src1 ? g0.ld1 : g0.ld0) * 2);
+  d.s0 = ph_rsrc(two ? g1.src0 : g0.src0, two ? (long long)p.M * g1.ld0 * 2 : 0);
+  d.s1 = ph_rsrc(two && g1.src1 ? g1.src1 : g0.src0, two && g1.src1 ? (long long)p.M * g1.ld1 * 2 : 0);
+  d.w = ph_rsrc(p.W, (long long)p.wrows * p.ldw * 2);
+  return d;
+}
+
+// Per-lane context of A row m (output pixel) for segment 0: pixb = source pixel index of
+// the tap window origin, msk = bit per in-image tap; upsample: pixb = b*h, msk = oy<<16|ox.
+__device__ __forceinline__ void a_row_ctx(const Params& p, int m, unsigned& pixb, unsigned& msk) {
+  const Seg& g0 = p.seg[0];
+  const bool valid = m < p.M;
+  const int mm = valid ? m : 0;
+  const int b = mm / p.hw_out, rem = mm - b * p.hw_out;
+  const int oy = rem / p.wo, ox = rem - oy * p.wo;
+  unsigned pb, mk = 0;
+  if (!g0.upsample) {
+    const int oys = oy * g0.stride, oxs = ox * g0.stride;
+    pb = (unsigned)((b * g0.h + oys) * g0.w + oxs);
+    for (int ky = 0; ky < g0.ksize; ++ky)
+      for (int kx = 0; kx < g0.ksize; ++kx) {
+        const int iy = oys + ky - g0.pad, ix = oxs + kx - g0.pad;
+        const bool in = valid & ((unsigned)iy < (unsigned)g0.h) & ((unsigned)ix < (unsigned)g0.w);
+        mk |= (in ? 1u : 0u) << (ky * g0.ksize + kx);
+      }
+  } else {
+    pb = (unsigned)(b * g0.h);
+    mk = valid ? ((unsigned)oy << 16 | (unsigned)ox) : 0x7fff7fffu;
+  }
+  pixb = pb;
+  msk = mk;
+}
+
+__device__ __forceinline__ unsigned w_row_ctx(const Params& p, int n, int rch) {
+  return n < p.wrows ? (unsigned)(n * p.ldw) * 2u + (unsigned)rch * 16u : PH_OOB;
+}
+
+// One 1-KiB A piece (8 rows x 64 channels) of K-step (seg, ky, kx, cb) into dst.
+__device__ __forceinline__ void dma_a_piece(const Params& p, const DmaSrc& d, half_t* dst, unsigned pixb,
+                                            unsigned msk, int m, int rch, int seg, int ky, int kx, int cb) {
+  const Seg& g0 = p.seg[0];
+  const Seg& g1 = p.seg[1];
+  const unsigned rch16 = (unsigned)rch * 16u;
+  if (seg == 0) {
+    const bool second = cb >= g0.c_split;
+    const __amdgpu_buffer_rsrc_t r = second ? d.a1 : d.a0;
+    const unsigned ld2 = (unsigned)(second ? g0.ld1 : g0.ld0) * 2u;
+    const int coff2 = (cb - (second ? g0.c_split : 0)) * 2;
+    const bool cok = (cb + BK <= g0.cin) || (cb + rch * 8 < g0.cin);
+    const int dy = ky - g0.pad, dx = kx - g0.pad;
+    unsigned off;
+    bool ok;
+    if (!g0.upsample) {
+      const int tapb = ky * g0.ksize + kx;
+      off = __umul24(pixb, ld2) + rch16 + (unsigned)((dy * g0.w + dx) * (int)ld2 + coff2);
+      ok = ((msk >> tapb) & 1u) && cok;
+    } else {
+      const int iy = (int)(msk >> 16) + dy, ix = (int)(msk & 0xffffu) + dx;
+      ok = ((unsigned)iy < 2u * g0.h) && ((unsigned)ix < 2u * g0.w) && cok;
+      const unsigned pix = (pixb + (unsigned)(iy >> 1)) * (unsigned)g0.w + (unsigned)(ix >> 1);
+      off = __umul24(pix, ld2) + rch16 + (unsigned)coff2;
+    }
+    ph_dma(r, dst, ok ? off : PH_OOB, 0);
+  } else {
+    const bool second = cb >= g1.c_split;
+    const __amdgpu_buffer_rsrc_t r = second ? d.s1 : d.s0;
+    const unsigned ld2 = (unsigned)(second ? g1.ld1 : g1.ld0) * 2u;
+    const unsigned coff2 = (unsigned)(cb - (second ? g1.c_split : 0)) * 2u;
+    const bool cok = (cb + BK <= g1.cin) || (cb + rch * 8 < g1.cin);
+    const bool ok = (m < p.M) && cok;
+    ph_dma(r, dst, ok ? __umul24((unsigned)m, ld2) + rch16 + coff2 : PH_OOB, 0);
+  }
+}
+
+// One (tile, K-split) work item per workgroup, two LDS stages.
 template <class CF>
 __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_glds_kernel(Params p) {
   extern __shared__ __attribute__((aligned(16))) half_t lds[];
@@ -505,91 +631,47 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_glds_kernel(Params p)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / CF::WN, wn = wave % CF::WN;
-  const int ntiles = p.tiles_m * p.tiles_n;
-  const int tile = xcd_remap(blockIdx.x, ntiles);
+  const int nitems = p.tiles_m * p.tiles_n * p.split;
+  // XCD-aware item order: neighbouring tiles (shared A rows / W rows) share an L2
+  const int it = xcd_remap((int)blockIdx.x + (int)blockIdx.y * (int)gridDim.x, nitems);
+  const int tile = it / p.split, sidx = it - tile * p.split;
   const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
   const int m0 = tm * CF::TBM, n0 = tn * CF::TBN;
-  const int kt0 = blockIdx.y * p.kt_per_split;
-  const int kt1 = min(p.kt_total, kt0 + p.kt_per_split);
-
-  // per-lane, per-instruction row context (fixed over the K loop): for A rows the
-  // output pixel (b, oy, ox); for W rows the weight row pointer.  Offsets into a
-  // source are 32-bit element counts (sources < 2^32 elements, checked on the host).
+  const int kt0 = sidx * p.kt_per_split, kt1 = min(p.kt_total, kt0 + p.kt_per_split);
   const int lrow = lane >> 3;
-  // A rows: ra[j] = (b << 16) | oy (oy = 0x7fff marks a row past M), rx[j] = ox;
-  // W rows: ra[j] = clamped weight row.  The swizzle chunk is recomputed per use.
-  int ra[GPW], rx[GPW];
+  const DmaSrc d = make_dma_src(p);
+  // per piece j (rows (j*NW + wave)*8 + lrow of the stage): A -> (pixb, msk), W -> byte offset
+  unsigned cx[GPW], cy[GPW];
 #pragma unroll
   for (int j = 0; j < GPW; ++j) {
-    const int R = (j * CF::NW + wave) * 8 + lrow;           // stage row (instruction j*NW + wave)
-    if ((j * CF::NW + wave) >= CF::NINSTR) {                // padding piece
-      ra[j] = rx[j] = 0;
-    } else if ((j * CF::NW + wave) * 8 < CF::TBM) {         // A row (wave-uniform per j)
-      const int m = m0 + R;
-      const int mm = m < p.M ? m : 0;
-      const int b = mm / p.hw_out, rem = mm - b * p.hw_out;
-      const int oy = rem / p.wo;
-      ra[j] = (b << 16) | (m < p.M ? oy : 0x7fff);
-      rx[j] = rem - oy * p.wo;
-    } else {
-      ra[j] = min(n0 + R - CF::TBM, p.wrows - 1);          // weight row (clamped; cols >= N discarded)
-      rx[j] = 0;
+    const int piece = j * CF::NW + wave;
+    const int rch = (lane & 7) ^ ((4 * piece + (lrow >> 1)) & 7);
+    unsigned x = PH_OOB, y = 0;
+    if (piece < CF::NINSTR) {
+      if (piece * 8 < CF::TBM) a_row_ctx(p, m0 + piece * 8 + lrow, x, y);
+      else x = w_row_ctx(p, n0 + piece * 8 + lrow - CF::TBM, rch);
     }
+    cx[j] = x;
+    cy[j] = y;
   }
-  const half_t* zero = g_zero_page;
-
-  // segment fields are read with constant indices only (uniform scalar selects): a
-  // dynamic index into the kernarg struct becomes vector loads whose s_waitcnt
-  // vmcnt(0) would drain the DMA in flight.
-  const int kt_b1 = p.nseg > 1 ? p.seg[1].kt_begin : 0x7fffffff;
-  auto stage = [&](int kt, int buf) {
-    const bool s1 = kt >= kt_b1;
-#define SEGF(f) (s1 ? p.seg[1].f : p.seg[0].f)
-    const int kt_begin = SEGF(kt_begin), tpt = SEGF(tiles_per_tap), ks = SEGF(ksize);
-    const int sh = SEGF(h), sw = SEGF(w), sstride = SEGF(stride), spad = SEGF(pad), sup = SEGF(upsample);
-    const int cin = SEGF(cin), csplit = SEGF(c_split), ld0 = SEGF(ld0), ld1 = SEGF(ld1), koff = SEGF(k_off);
-    const half_t* src0 = SEGF(src0);
-    const half_t* src1 = SEGF(src1);
-#undef SEGF
-    const int local = kt - kt_begin;
-    const int tap = local / tpt;
-    const int cbase = (local - tap * tpt) * BK;
-    const int ky = tap / ks, kx = tap - ky * ks;
-    const int kcol = koff + local * BK;
-    const unsigned lh = sup ? 2 * sh : sh, lw = sup ? 2 * sw : sw;
-    const int dy = ky - spad, dx = kx - spad;
-#pragma unroll
-    for (int j = 0; j < GPW; ++j) {
-      const int rbase = (j * CF::NW + wave) * 8;
-      const bool pad_piece = (j * CF::NW + wave) >= CF::NINSTR;
-      __attribute__((address_space(3))) void* dst =
-          (__attribute__((address_space(3))) void*)(pad_piece ? lds + 2 * CF::STAGE_H
-                                                              : lds + buf * CF::STAGE_H + rbase * BK);
-      const half_t* src;
-      const int rchunk = (lane & 7) ^ (((rbase >> 1) + (lrow >> 1)) & 7);
-      if (pad_piece) {
-        src = zero;
-      } else if (rbase < CF::TBM) {
-        const int c = cbase + rchunk * 8;
-        const int oy = ra[j] & 0xffff, bimg = ra[j] >> 16;
-        int iy = (oy == 0x7fff) ? -1 : oy * sstride + dy;
-        int ix = rx[j] * sstride + dx;
-        const bool in = (c < cin) & ((unsigned)iy < lh) & ((unsigned)ix < lw);
-        iy >>= sup;
-        ix >>= sup;
-        const bool second = c >= csplit;
-        const unsigned ld = second ? ld1 : ld0;
-        const unsigned cc = second ? c - csplit : c;
-        const half_t* base = second ? src1 : src0;
-        const unsigned pix = ((unsigned)(bimg * sh + iy)) * (unsigned)sw + (unsigned)ix;
-        const unsigned off = pix * ld + cc;
-        src = in ? base + off : zero;
-      } else {
-        src = p.W + (size_t)ra[j] * p.ldw + kcol + rchunk * 8;
-      }
-      __builtin_amdgcn_global_load_lds((const void*)src, dst, 16, 0, 0);
-    }
-  };
+  int sg, ky, kx, cb;
+  ph_kstate(p, kt0, sg, ky, kx, cb);
+#define SDK_STAGE(KT_, BUF_)                                                                 \
+  do {                                                                                       \
+    _Pragma("unroll") for (int j = 0; j < GPW; ++j) {                                        \
+      const int piece = j * CF::NW + wave;                                                   \
+      const int rch = (lane & 7) ^ ((4 * piece + (lrow >> 1)) & 7);                          \
+      if (piece >= CF::NINSTR) {                                                             \
+        ph_dma(d.w, lds + 2 * CF::STAGE_H, PH_OOB, 0);                                       \
+      } else if (piece * 8 < CF::TBM) {                                                      \
+        dma_a_piece(p, d, lds + (BUF_) * CF::STAGE_H + piece * 8 * BK, cx[j], cy[j],         \
+                    m0 + piece * 8 + lrow, rch, sg, ky, kx, cb);                             \
+      } else {                                                                               \
+        ph_dma(d.w, lds + (BUF_) * CF::STAGE_H + piece * 8 * BK, cx[j], (KT_) * BK * 2);     \
+      }                                                                                      \
+    }                                                                                        \
+    ph_kadv(p, sg, ky, kx, cb);                                                              \
+  } while (0)
 
   f16v acc[CF::FM][CF::FN];
 #pragma unroll
@@ -600,11 +682,12 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_glds_kernel(Params p)
   const int fr = lane & 31, fh = lane >> 5;
   const int arow0 = wm * CF::TM + fr;
   const int brow0 = CF::TBM + wn * CF::TN + fr;
-  if (kt0 < kt1) stage(kt0, 0);
+
+  SDK_STAGE(kt0, 0);
+  int buf = 0;
   for (int kt = kt0; kt < kt1; ++kt) {
-    const int cur = (kt - kt0) & 1;
     if (kt + 1 < kt1) {
-      stage(kt + 1, cur ^ 1);
+      SDK_STAGE(kt + 1, buf ^ 1);
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPW) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -612,7 +695,7 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_glds_kernel(Params p)
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    const half_t* st = lds + cur * CF::STAGE_H;
+    const half_t* st = lds + buf * CF::STAGE_H;
 #pragma unroll
     for (int kk = 0; kk < BK / 16; ++kk) {
       h8 fa[CF::FM], fb[CF::FN];
@@ -629,11 +712,12 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_glds_kernel(Params p)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[j], fa[i], acc[i][j], 0, 0, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();      // everyone done reading `cur` before it is restaged
+    __builtin_amdgcn_s_barrier();      // everyone done reading `buf` before it is restaged
     __builtin_amdgcn_sched_barrier(0);
+    buf ^= 1;
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  epilogue_direct<CF::FM, CF::FN>(p, acc, m0, n0, wm * CF::TM, wn * CF::TN, blockIdx.y);
+#undef SDK_STAGE
+  epilogue_direct<CF::FM, CF::FN>(p, acc, m0, n0, wm * CF::TM, wn * CF::TN, sidx);
 }
 
 using Cfg256x256 = Cfg<256, 256, 2, 4>;
@@ -643,6 +727,228 @@ using Cfg128x128 = Cfg<128, 128, 2, 2>;
 using Cfg256x320 = Cfg<256, 320, 8, 2>;   // 16 waves
 using Cfg256x160 = Cfg<256, 160, 8, 1>;
 using Cfg128x320 = Cfg<128, 320, 4, 2>;
+
+// ---------------------------------------------------------------------- phased LDS-DMA kernel
+// 256x256 tile, 8 waves (2 x 4), K-step 64 cut into four 16-KiB half-tiles streamed in
+// the order A0 (pixels 0-127), W0 (even 32-channel groups), W1 (odd groups), A1
+// (pixels 128-255).  One phase multiplies one (A half, W half) quadrant: 8 MFMAs per
+// wave, fragments for the phase read from LDS at its start; a phase is two sections
+// (reads + DMA issue + address math | MFMAs) separated by barriers, and the two wave
+// rows run one barrier apart (ping-pong) so each SIMD overlaps one wave's MFMAs with
+// the other wave's loads.
+// Each phase issues the DMA of the half-tile D phases ahead into a ring of S slots
+// (S >= D + 2: a slot is refilled >= 2 phases after its last read, which covers the
+// one-barrier skew of the wave rows), and waits with a
+// counted vmcnt that leaves D-2 (or D-1) half-tiles in flight — the loads of the next
+// K-steps stream under the MFMAs instead of once per K-step behind a full barrier.
+// Past the last K-step the same slots receive zero-page DMAs so every phase keeps
+// the same vmcnt immediates.  A wave owns pixels {a*128 + wr*64 + (0..63)} and
+// channels {64*wc + 32*b + (0..31)}, so a GEGLU (x, gate) 32-channel pair sits in one
+// wave (W0 / W1 halves) and the direct epilogue applies unchanged.
+template <int S_, int D_>
+struct PhCfg {
+  static constexpr int S = S_, D = D_;
+  static constexpr int LDS_BYTES = S * 128 * BK * 2;
+  static_assert(S >= D + 2 && D >= 2 && LDS_BYTES <= 160 * 1024, "ring too small / too large");
+};
+constexpr int PH_HALF = 128 * BK;   // halfs per half-tile slot
+
+template <class PC, int DBG = 0>
+__global__ void __launch_bounds__(512) conv_ph_kernel(Params p) {
+  extern __shared__ __attribute__((aligned(16))) half_t lds[];
+  constexpr int S = PC::S, D = PC::D;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int nitems = p.tiles_m * p.tiles_n * p.split;
+  const int it = xcd_remap((int)blockIdx.x + (int)blockIdx.y * (int)gridDim.x, nitems);
+  const int tile = it / p.split, sidx = it - tile * p.split;
+  const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int kt0 = sidx * p.kt_per_split, kt1 = min(p.kt_total, kt0 + p.kt_per_split);
+  const int nk = kt1 - kt0;
+  const int lrow = lane >> 3;
+  const int rch = (lane & 7) ^ ((wave * 4 + (lrow >> 1)) & 7);
+
+  const DmaSrc d = make_dma_src(p);
+  // this lane's DMA rows: slot row j*64 + wave*8 + lrow of every half (q = half*2 + j)
+  unsigned pixb[4], msk[4], wv[4];
+  const int mrow = m0 + wave * 8 + lrow;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int a = q >> 1, j = q & 1;
+    a_row_ctx(p, mrow + a * 128 + j * 64, pixb[q], msk[q]);
+    const int pc = j * 8 + wave;
+    wv[q] = w_row_ctx(p, n0 + 64 * (pc >> 2) + 32 * a + 8 * (pc & 3) + lrow, rch);
+  }
+
+#define SDK_PH_ISSUE_A(A_, SEG, KY, KX, CB, T, SLOT)                                       \
+  do {                                                                                     \
+    half_t* sl_ = lds + (SLOT) * PH_HALF + wave * 8 * BK;                                  \
+    const int kt_ = kt0 + (T);                                                             \
+    if (DBG & 1) {                                                                         \
+    } else if (kt_ >= kt1) {                                                               \
+      _Pragma("unroll") for (int j = 0; j < 2; ++j) ph_dma(d.w, sl_ + j * 64 * BK, PH_OOB, 0); \
+    } else {                                                                               \
+      _Pragma("unroll") for (int j = 0; j < 2; ++j)                                        \
+        dma_a_piece(p, d, sl_ + j * 64 * BK, pixb[(A_) * 2 + j], msk[(A_) * 2 + j],         \
+                    mrow + (A_) * 128 + j * 64, rch, SEG, KY, KX, CB);                     \
+    }                                                                                      \
+  } while (0)
+#define SDK_PH_ISSUE_W(B_, T, SLOT)                                                        \
+  do {                                                                                     \
+    half_t* sl_ = lds + (SLOT) * PH_HALF + wave * 8 * BK;                                  \
+    const int kt_ = kt0 + (T);                                                             \
+    if (DBG & 1) {                                                                         \
+    } else if (kt_ >= kt1) {                                                               \
+      _Pragma("unroll") for (int j = 0; j < 2; ++j) ph_dma(d.w, sl_ + j * 64 * BK, PH_OOB, 0); \
+    } else {                                                                               \
+      _Pragma("unroll") for (int j = 0; j < 2; ++j)                                        \
+        ph_dma(d.w, sl_ + j * 64 * BK, wv[(B_) * 2 + j], kt_ * BK * 2);                    \
+    }                                                                                      \
+  } while (0)
+
+  // prologue: half-tiles 0 .. D-1 (K-state decoded directly)
+#pragma unroll
+  for (int h = 0; h < D; ++h) {
+    const int idx = h & 3;
+    if (idx == 1 || idx == 2) {
+      SDK_PH_ISSUE_W(idx - 1, h >> 2, h % S);
+    } else {
+      int sg, ky, kx, cb;
+      ph_kstate(p, kt0 + (h >> 2), sg, ky, kx, cb);
+      SDK_PH_ISSUE_A(idx == 3 ? 1 : 0, sg, ky, kx, cb, h >> 2, h % S);
+    }
+  }
+  // in-loop A K-states: A0 / A1 half-tiles are issued for K-step t + TO0 / t + TO1
+  constexpr int Q0 = ((0 - D) % 4 + 4) % 4, TO0 = (Q0 + D) >> 2;
+  constexpr int Q3 = ((3 - D) % 4 + 4) % 4, TO3 = (Q3 + D) >> 2;
+  int a0g, a0y, a0x, a0c, a1g, a1y, a1x, a1c;
+  ph_kstate(p, kt0 + TO0, a0g, a0y, a0x, a0c);
+  ph_kstate(p, kt0 + TO3, a1g, a1y, a1x, a1c);
+#define SDK_PH_ISSUE(IDX, T, SLOT)                                                         \
+  do {                                                                                     \
+    if ((IDX) == 0) {                                                                      \
+      SDK_PH_ISSUE_A(0, a0g, a0y, a0x, a0c, T, SLOT);                                      \
+      ph_kadv(p, a0g, a0y, a0x, a0c);                                                      \
+    } else if ((IDX) == 3) {                                                               \
+      SDK_PH_ISSUE_A(1, a1g, a1y, a1x, a1c, T, SLOT);                                      \
+      ph_kadv(p, a1g, a1y, a1x, a1c);                                                      \
+    } else {                                                                               \
+      SDK_PH_ISSUE_W((IDX) - 1, T, SLOT);                                                  \
+    }                                                                                      \
+  } while (0)
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (D - 2)) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+
+  f16v acc[2][2][2];   // [A half][pixel tile][W half]
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) acc[a][i][b] = f16v{};
+  const int fr = lane & 31, fh = lane >> 5;
+  h8 fa[2][4], fb0[4], fb1[4];
+#define SDK_PH_READ_A(SLOT)                                                                \
+  do {                                                                                     \
+    const half_t* s_ = lds + (SLOT) * PH_HALF;                                             \
+    _Pragma("unroll") for (int i = 0; i < 2; ++i)                                          \
+      _Pragma("unroll") for (int kk = 0; kk < 4; ++kk)                                     \
+        fa[i][kk] = *reinterpret_cast<const h8*>(s_ + swz(wr * 64 + i * 32 + fr, kk * 2 + fh)); \
+  } while (0)
+#define SDK_PH_READ_B(FB, SLOT)                                                            \
+  do {                                                                                     \
+    const half_t* s_ = lds + (SLOT) * PH_HALF;                                             \
+    _Pragma("unroll") for (int kk = 0; kk < 4; ++kk)                                       \
+      FB[kk] = *reinterpret_cast<const h8*>(s_ + swz(wc * 32 + fr, kk * 2 + fh));           \
+  } while (0)
+#define SDK_PH_SYNC(NOUT)                                                                  \
+  do {                                                                                     \
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (NOUT)) : "memory");                      \
+    __builtin_amdgcn_sched_barrier(0);                                                     \
+    __builtin_amdgcn_s_barrier();                                                          \
+    __builtin_amdgcn_sched_barrier(0);                                                     \
+  } while (0)
+#define SDK_PH_MMA(A, FB)                                                                  \
+  do {                                                                                     \
+    __builtin_amdgcn_s_setprio(1);                                                         \
+    if (!(DBG & 2)) _Pragma("unroll") for (int kk = 0; kk < 4; ++kk)                       \
+      _Pragma("unroll") for (int i = 0; i < 2; ++i)                                        \
+        acc[A][i][(FB) == 1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(                     \
+            (FB) ? fb1[kk] : fb0[kk], fa[i][kk], acc[A][i][(FB) == 1], 0, 0, 0);           \
+    __builtin_amdgcn_s_setprio(0);                                                         \
+  } while (0)
+
+#define SDK_PH_BAR()                                                                       \
+  do {                                                                                     \
+    __builtin_amdgcn_sched_barrier(0);                                                     \
+    __builtin_amdgcn_s_barrier();                                                          \
+    __builtin_amdgcn_sched_barrier(0);                                                     \
+  } while (0)
+  // ping-pong: the wr = 1 waves run one barrier behind, so on every SIMD one wave's
+  // MFMA section overlaps the other wave's fragment reads / DMA issue / address math
+  if (wr == 1) SDK_PH_BAR();
+  for (int t = 0; t < nk; ++t) {
+    const int g = 4 * t;
+    // phase 0: (A0, W0)
+    SDK_PH_READ_A(g % S);
+    SDK_PH_READ_B(fb0, (g + 1) % S);
+    SDK_PH_ISSUE((0 + D) & 3, (g + 0 + D) >> 2, (g + 0 + D) % S);
+    SDK_PH_SYNC(D - 2);
+    SDK_PH_MMA(0, 0);
+    SDK_PH_BAR();
+    // phase 1: (A0, W1)
+    SDK_PH_READ_B(fb1, (g + 2) % S);
+    SDK_PH_ISSUE((1 + D) & 3, (g + 1 + D) >> 2, (g + 1 + D) % S);
+    SDK_PH_SYNC(D - 2);
+    SDK_PH_MMA(0, 1);
+    SDK_PH_BAR();
+    // phase 2: (A1, W1)
+    SDK_PH_READ_A((g + 3) % S);
+    SDK_PH_ISSUE((2 + D) & 3, (g + 2 + D) >> 2, (g + 2 + D) % S);
+    SDK_PH_SYNC(D - 1);
+    SDK_PH_MMA(1, 1);
+    SDK_PH_BAR();
+    // phase 3: (A1, W0) — fragments already in registers
+    SDK_PH_ISSUE((3 + D) & 3, (g + 3 + D) >> 2, (g + 3 + D) % S);
+    SDK_PH_SYNC(D - 2);
+    SDK_PH_MMA(1, 0);
+    SDK_PH_BAR();
+  }
+  if (wr == 0) SDK_PH_BAR();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#undef SDK_PH_BAR
+#undef SDK_PH_ISSUE
+#undef SDK_PH_ISSUE_A
+#undef SDK_PH_ISSUE_W
+#undef SDK_PH_READ_A
+#undef SDK_PH_READ_B
+#undef SDK_PH_SYNC
+#undef SDK_PH_MMA
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+    epilogue_direct<2, 2>(p, acc[a], m0, n0, a * 128 + wr * 64, wc * 64, sidx);
+}
+
+using PhCfg8 = PhCfg<8, 6>;
+using PhCfg10 = PhCfg<10, 8>;
+
+template <class PC, int DBG = 0>
+int launch_ph(const Params& p, hipStream_t s) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    if (hipFuncSetAttribute((const void*)conv_ph_kernel<PC, DBG>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            PC::LDS_BYTES) != hipSuccess)
+      return fail(SDK_EHIP, "conv2d: cannot raise the dynamic LDS limit");
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((conv_ph_kernel<PC, DBG>), dim3(p.tiles_m * p.tiles_n, p.split), dim3(512), PC::LDS_BYTES,
+                     s, p);
+  return check_launch("conv_ph");
+}
 
 // Split-K reduction + epilogue: 8 columns per thread.
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(Params p) {
@@ -691,7 +997,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(Params p) {
 }
 
 template <class CF>
-int launch_glds(const Params& p, dim3 grid, hipStream_t s) {
+int launch_glds(const Params& p, hipStream_t s) {
   static bool attr_set = false;   // raise the dynamic-LDS cap once per instantiation (not a per-call alloc)
   if (!attr_set) {
     if (hipFuncSetAttribute((const void*)conv_glds_kernel<CF>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -699,7 +1005,8 @@ int launch_glds(const Params& p, dim3 grid, hipStream_t s) {
       return fail(SDK_EHIP, "conv2d: cannot raise the dynamic LDS limit");
     attr_set = true;
   }
-  hipLaunchKernelGGL(conv_glds_kernel<CF>, grid, dim3(CF::NT), CF::LDS_BYTES, s, p);
+  hipLaunchKernelGGL((conv_glds_kernel<CF>), dim3(p.tiles_m * p.tiles_n, p.split), dim3(CF::NT), CF::LDS_BYTES, s,
+                     p);
   return check_launch("conv_glds");
 }
 
@@ -755,15 +1062,20 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   for (int s = 0; s < a->nseg; ++s) {
     const sdk_conv_src& g = a->seg[s];
     transform |= (g.gn_scale != nullptr) || g.silu;
-    // the LDS-DMA kernels address sources with 32-bit element offsets
-    if ((double)a->batch * g.h * g.w * std::max(g.ld0, g.ld1) >= 4294967296.0) transform = true;
+    // the LDS-DMA kernels: buffer resources (31-bit byte offsets), a K-step's 64 channels
+    // from one concat source, and a second segment that is a plain 1x1 over the output grid
+    if ((double)a->batch * g.h * g.w * std::max(g.ld0, g.ld1) * 2 >= 2147483647.0) transform = true;
+    if (g.c_split < g.cin && g.c_split % BK) transform = true;
+    if (s == 1 && (g.ksize != 1 || g.stride != 1 || g.pad != 0 || g.upsample || g.h != a->ho || g.w != a->wo))
+      transform = true;
   }
+  if ((double)((a->cout + 127) / 128 * 128) * a->k_total * 2 >= 2147483647.0) transform = true;
   // tile configuration: LDS-DMA kernels for transform-free operands, scored by
   // padded-work efficiency x whole-chip wave quantisation x measured per-config
   // throughput
   struct Opt { int variant, bm, bn, nw; double pref; bool geglu_ok; };
   // relative throughput of each config on shapes it tiles exactly (tools/bench_conv.py, MI355X)
-  const Opt opts[] = {{2, 256, 256, 8, 1.00, true}, {5, 256, 320, 16, 0.92, false},
+  const Opt opts[] = {{8, 256, 256, 8, 1.05, true}, {2, 256, 256, 8, 1.00, true}, {5, 256, 320, 16, 0.92, false},
                       {7, 128, 320, 8, 0.88, false}, {6, 256, 160, 8, 0.72, false},
                       {4, 128, 128, 4, 0.72, true}, {3, 256, 128, 8, 0.65, true}};
   int var = 0, tbm = BM, tbn = BN, best_split = 0;
@@ -803,13 +1115,16 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   // benchmarks, SDK_CONV_VARIANT=id
   const char* fe = getenv("SDK_CONV_VARIANT");
   const int forced = a->variant_hint > 0 ? a->variant_hint - 1 : (fe ? atoi(fe) : -1);
-  if (forced >= 0 && forced <= 7 && forced != 1 && (forced == 0 || !transform) &&
-      !(forced >= 5 && a->out_mode == SDK_OUT_GEGLU_F16)) {
-    static const int fbm[8] = {128, 0, 256, 256, 128, 256, 256, 128};
-    static const int fbn[8] = {128, 0, 256, 128, 128, 320, 160, 320};
+  // ids: 0 register-staged; 2..7 LDS-DMA configs; 8, 9 phased 256x256; 10.. diagnostics
+  const int fbase = forced;
+  const bool fvalid = forced >= 0 && forced != 1 && forced <= 15;
+  const bool fgeglu = fbase <= 4 || fbase >= 8;
+  if (fvalid && (forced == 0 || !transform) && (fgeglu || a->out_mode != SDK_OUT_GEGLU_F16)) {
+    static const int fbm[16] = {128, 0, 256, 256, 128, 256, 256, 128, 256, 256, 256, 256, 256, 256, 256, 256};
+    static const int fbn[16] = {128, 0, 256, 128, 128, 320, 160, 320, 256, 256, 256, 256, 256, 256, 256, 256};
     var = forced;
-    tbm = fbm[forced];
-    tbn = fbn[forced];
+    tbm = fbm[fbase];
+    tbn = fbn[fbase];
     best_split = 0;
   }
   p.variant = var;
@@ -817,7 +1132,7 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   p.tiles_n = (p.N + tbn - 1) / tbn;
   p.Npad = p.tiles_n * tbn;                       // split-K slab row stride
   const int tiles = p.tiles_m * p.tiles_n;
-  const int per_cu = (var == 0 || var == 4) ? 2 : 1;
+  const int per_cu = ((var & 15) == 0 || (var & 15) == 4) ? 2 : 1;
   int split = a->split_k;
   if (split <= 0) {
     if (best_split > 0) {
@@ -867,12 +1182,20 @@ extern "C" int sdk_conv2d(const sdk_conv_args* a, sdk_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
   dim3 grid(p.tiles_m * p.tiles_n, p.split);
   switch (p.variant) {
-    case 2: rc = launch_glds<Cfg256x256>(p, grid, s); break;
-    case 3: rc = launch_glds<Cfg256x128>(p, grid, s); break;
-    case 4: rc = launch_glds<Cfg128x128>(p, grid, s); break;
-    case 5: rc = launch_glds<Cfg256x320>(p, grid, s); break;
-    case 6: rc = launch_glds<Cfg256x160>(p, grid, s); break;
-    case 7: rc = launch_glds<Cfg128x320>(p, grid, s); break;
+    case 2: rc = launch_glds<Cfg256x256>(p, s); break;
+    case 3: rc = launch_glds<Cfg256x128>(p, s); break;
+    case 4: rc = launch_glds<Cfg128x128>(p, s); break;
+    case 5: rc = launch_glds<Cfg256x320>(p, s); break;
+    case 6: rc = launch_glds<Cfg256x160>(p, s); break;
+    case 7: rc = launch_glds<Cfg128x320>(p, s); break;
+    case 8: rc = launch_ph<PhCfg8>(p, s); break;
+    case 9: rc = launch_ph<PhCfg10>(p, s); break;
+    case 10: rc = launch_ph<PhCfg8, 1>(p, s); break;   // diagnostics: no DMA
+    case 11: rc = launch_ph<PhCfg8, 2>(p, s); break;   // diagnostics: no MFMA
+    case 12: rc = launch_ph<PhCfg8, 4>(p, s); break;   // diagnostics: DMA from the zero page
+    case 13: rc = launch_ph<PhCfg8, 8>(p, s); break;   // diagnostics: every tile reads tile 0's footprint
+    case 14: rc = launch_ph<PhCfg8, 16>(p, s); break;  // diagnostics: W from the zero page
+    case 15: rc = launch_ph<PhCfg8, 32>(p, s); break;  // diagnostics: A from the zero page
     default:
       hipLaunchKernelGGL(conv_igemm_kernel, grid, dim3(NT), 0, s, p);
       rc = check_launch("conv_igemm");

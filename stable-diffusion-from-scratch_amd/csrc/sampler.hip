@@ -169,6 +169,8 @@ extern "C" const char* sdk_kernel_name(int32_t variant) {
     case 5: return "conv_glds_kernel<Cfg<256,320,8,2>>";
     case 6: return "conv_glds_kernel<Cfg<256,160,8,1>>";
     case 7: return "conv_glds_kernel<Cfg<128,320,4,2>>";
+    case 8: return "conv_ph_kernel<256x256,ring8>";
+    case 9: return "conv_ph_kernel<256x256,ring10>";
     default: return "unknown";
   }
 }

@@ -163,7 +163,7 @@ class _Autotune:
     Enabled by ``enable()`` (UNetModel/AutoEncoderKL.prepare(autotune=True)); the
     first call of each distinct problem times every candidate (HIP events, 3 reps
     after a warm-up) and caches the fastest.  Never runs under graph capture."""
-    VARIANTS = (2, 5, 7, 6, 4, 3)
+    VARIANTS = (2, 5, 7, 6, 4, 3, 8, 9)
     SPLITS = (0, 1, 2, 4, 8)
 
     def __init__(self):
@@ -218,9 +218,12 @@ AUTOTUNE = _Autotune()
 
 
 def conv2d(pc: PackedConv, x, *, ksize=None, stride=1, pad=None, upsample=False, gn=None, silu=False,
-           seg2=None, bias=True, row_bias=None, residual=None, out_mode=OUT_NHWC_F16, out=None):
+           seg2=None, bias=True, row_bias=None, residual=None, out_mode=OUT_NHWC_F16, out=None,
+           variant=None, split_k=None):
     """Run the implicit-GEMM conv.  ``seg2`` = (x2, gn2, silu2) adds a fused 1x1 K segment.
-    ``row_bias`` = (fp32 tensor [B, ld], column offset) — the per-(batch, channel) add."""
+    ``row_bias`` = (fp32 tensor [B, ld], column offset) — the per-(batch, channel) add.
+    ``variant`` / ``split_k`` force a kernel configuration (benchmarks; default: planner
+    or autotuner)."""
     a = ConvArgs()
     k0 = pc.seg_geom[0][0] if ksize is None else ksize
     if pad is None:
@@ -262,6 +265,10 @@ def conv2d(pc: PackedConv, x, *, ksize=None, stride=1, pad=None, upsample=False,
     tuned = AUTOTUNE.choose(a, pc, dev) if (AUTOTUNE.enabled or AUTOTUNE.table) else None
     if tuned is not None:
         a.variant_hint, a.split_k = tuned
+    if variant is not None:
+        a.variant_hint = variant + 1
+    if split_k is not None:
+        a.split_k = split_k
     info = ConvPlanInfo()
     check(lib().sdk_conv2d_plan(C.byref(a), C.byref(info)), "conv2d_plan")
     if info.workspace_bytes > 0:

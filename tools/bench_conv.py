@@ -63,7 +63,7 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "child":
         child()
     else:
-        variants = [int(v) for v in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["0", "2", "3", "4", "5", "6", "7", "-1"])]
+        variants = [int(v) for v in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["2", "3", "4", "5", "6", "7", "8", "-1"])]
         table = {v: run(v) for v in variants}
         names = [s[0] for s in SHAPES]
         print("shape".ljust(24) + "".join(f"v{v}".rjust(9) for v in variants))
