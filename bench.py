@@ -58,7 +58,7 @@ def synth_init_(module, seed, device):
             p.data = torch.ones(p.shape, device=device)
 
 
-def build_models(cfg, device):
+def build_models(cfg, device, graph=False):
     import sd_amd_loader
     sd_amd_loader.load()
     from sd_amd.openai_model.model import UNetModel
@@ -74,6 +74,8 @@ def build_models(cfg, device):
     unet.prepare(device)
     vae.prepare(device)
     sch = register_schedule(1000, 0.00085, 0.012)
+    from sd_amd.graphs import GraphedUNet
+    graphed = GraphedUNet(unet)
 
     class LatentModel:
         """LatentDiffusion.apply_model / decode_first_stage semantics (Diffusion/ddpm.py)."""
@@ -84,8 +86,11 @@ def build_models(cfg, device):
 
         def __init__(self):
             self.device = device
+            self.graph = graph
 
         def apply_model(self, x, t, c):
+            if self.graph:
+                return graphed(x, t, c)
             return unet(x, t, context=c)
 
         def decode_first_stage(self, z):
@@ -146,6 +151,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-autotune", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one HIP graph per UNet step")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -162,7 +168,7 @@ def main():
     B = args.batch or cfg["batch"]
     L = cfg["latent"]
 
-    unet, vae, model = build_models(cfg, device)
+    unet, vae, model = build_models(cfg, device, graph=not args.no_graph)
     from sd_amd.DDIM.ddim import DDIMSampler
     from sd_amd import ops
     sampler = DDIMSampler(model)
@@ -190,20 +196,23 @@ def main():
             tdist.barrier()
         torch.cuda.synchronize()
 
-    # the first warm-up step also autotunes every distinct conv problem (tile config x split-K)
+    # the first warm-up step also autotunes every distinct conv problem (tile config x split-K);
+    # the UNet graph is captured on its first graphed call, after the eager autotuning call
     ops.AUTOTUNE.enable(not args.no_autotune)
-    for _ in range(args.warmup):
-        one_step()
+    model.graph = False
+    one_step()
     ops.AUTOTUNE.enable(False)
+    model.graph = not args.no_graph
+    if model.graph:                      # capture the UNet graph (setup, not a sampling step)
+        model.apply_model(xT, torch.full((B,), 999, dtype=torch.long, device=device), ctx)
+    for _ in range(max(args.warmup - 1, 0)):
+        one_step()
     barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        if i == args.steps - 1 and not args.no_roofline:
-            ops.PROFILER.start()
         img = one_step()
     barrier()
     elapsed = time.perf_counter() - t0
-    ops.PROFILER.stop()
     if dist:
         import torch.distributed as tdist
         tt = torch.tensor([elapsed], device=device)
@@ -211,18 +220,30 @@ def main():
         elapsed = tt.item()
     finite = bool(torch.isfinite(img).all().item())
 
-    # UNet step latency at the config batch (HIP events around one forward)
+    # UNet step latency at the config batch (HIP events around replays of the sampler's UNet call)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     tts = torch.full((B,), 501, dtype=torch.long, device=device)
-    unet(xT, tts, ctx)
+    model.apply_model(xT, tts, ctx)
     torch.cuda.synchronize()
     e0.record()
     nrep = 5
     for _ in range(nrep):
-        unet(xT, tts, ctx)
+        model.apply_model(xT, tts, ctx)
     e1.record()
     torch.cuda.synchronize()
     unet_ms = e0.elapsed_time(e1) / nrep
+
+    # per-kernel breakdown: one extra, untimed, eager step on rank 0 with HIP events
+    # around every launch (not part of `value`)
+    if not args.no_roofline and rank == 0:
+        model.graph = False
+        ops.PROFILER.start()
+        z, _ = sampler.sample(S=args.ddim_steps, batch_size=B, shape=(4, L, L), conditioning=ctx, eta=0.0, x_T=xT,
+                              verbose=False, log_every_t=10 ** 9)
+        model.decode_first_stage(z)
+        torch.cuda.synchronize()
+        ops.PROFILER.stop()
+        model.graph = not args.no_graph
 
     images = world * B * args.steps
     value = images / elapsed
@@ -233,7 +254,7 @@ def main():
            "config": {"workload": cfg["workload"], "global_batch": world * B, "batch_per_gpu": B,
                       "latent": [4, L, L], "image": [3, 8 * L, 8 * L], "ddim_steps": args.ddim_steps, "eta": 0.0,
                       "parallelism": f"dp{world}", "collective": "all_gather decoded images (RCCL)" if dist else None},
-           "unet_step_ms": round(unet_ms, 3), "finite": finite,
+           "unet_step_ms": round(unet_ms, 3), "finite": finite, "hip_graph": not args.no_graph,
            "autotuned_conv_problems": len(ops.AUTOTUNE.table)}
     if not args.no_roofline and rank == 0:
         summ = ops.PROFILER.summary()
@@ -250,7 +271,7 @@ def main():
                                "kernel": "conv_igemm_kernel (+splitk_reduce_kernel on split-K launches)",
                                "launches": conv["launches"], "avg_launch_us": round(1e6 * avg_s, 2),
                                "flops_per_launch": conv["flops"] / conv["launches"]}
-        out["kernel_time_ms_last_step"] = {k: round(v["ms"], 2) for k, v in summ.items()}
+        out["kernel_time_ms_profiled_step"] = {k: round(v["ms"], 2) for k, v in summ.items()}
         if os.environ.get("BENCH_SHAPES_OUT"):
             with open(os.environ["BENCH_SHAPES_OUT"], "w") as f:
                 for (kind, shape), n, ms, tf in ops.PROFILER.shape_table():

@@ -85,30 +85,75 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnParams p) {
   const int vrow_off = 4 * (g >> 1) + q4;
   const int vcol_off = 16 * (g & 1) + 4 * pp;
 
-  for (int t = 0; t < ntiles; ++t) {
-    const int key0 = t * KT;
-    __syncthreads();   // previous tile fully consumed
-    for (int e = tid; e < KT * (DQK / 8); e += 256) {
-      const int kr = e / (DQK / 8), c = e - kr * (DQK / 8);
-      const int key = key0 + kr, dd = c * 8;
+  // K/V tiles are prefetched into registers one tile ahead (issue-early / write-late):
+  // the global loads of tile t+1 are in flight while tile t is multiplied
+  constexpr int KV_K = (KT * (DQK / 8) + 255) / 256, KV_V = (KT * (DV / 8) + 255) / 256;
+  h8 pk_k[KV_K], pk_v[KV_V];
+  auto fetch = [&](int key0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < KV_K; ++i) {
+      const int e = tid + 256 * i;
+      const int kr = e / (DQK / 8), dd = (e - kr * (DQK / 8)) * 8;
+      const int key = key0 + kr;
       h8 v = {};
-      if (key < p.nk && dd < p.d) v = *reinterpret_cast<const h8*>(kbase + (size_t)key * p.k_ld + dd);
-      *reinterpret_cast<h8*>(Ks + kr * KLD + dd) = v;
+      if (e < KT * (DQK / 8) && key < p.nk && dd < p.d) v = *reinterpret_cast<const h8*>(kbase + (size_t)key * p.k_ld + dd);
+      pk_k[i] = v;
     }
-    for (int e = tid; e < KT * (DV / 8); e += 256) {
-      const int kr = e / (DV / 8), c = e - kr * (DV / 8);
-      const int key = key0 + kr, dd = c * 8;
+#pragma unroll
+    for (int i = 0; i < KV_V; ++i) {
+      const int e = tid + 256 * i;
+      const int kr = e / (DV / 8), dd = (e - kr * (DV / 8)) * 8;
+      const int key = key0 + kr;
       h8 v = {};
-      if (key < p.nk) {
+      if (e < KT * (DV / 8) && key < p.nk) {
         if (dd + 8 <= p.d) {
           v = *reinterpret_cast<const h8*>(vbase + (size_t)key * p.v_ld + dd);
         } else if (ones_row && dd <= p.d && p.d < dd + 8) {
           v[p.d - dd] = (half_t)1.0f;       // ones column -> row sum of P in O^T row d
         }
       }
-      *reinterpret_cast<h8*>(Vs + kr * VLD + dd) = v;
+      pk_v[i] = v;
+    }
+  };
+  constexpr bool PREFETCH = DV <= 128;   // d = 160 has no registers to spare
+  if (PREFETCH) fetch(0);
+  for (int t = 0; t < ntiles; ++t) {
+    const int key0 = t * KT;
+    __syncthreads();   // previous tile fully consumed
+    if (!PREFETCH) {
+      for (int e = tid; e < KT * (DQK / 8); e += 256) {
+        const int kr = e / (DQK / 8), dd = (e - kr * (DQK / 8)) * 8;
+        const int key = key0 + kr;
+        h8 v = {};
+        if (key < p.nk && dd < p.d) v = *reinterpret_cast<const h8*>(kbase + (size_t)key * p.k_ld + dd);
+        *reinterpret_cast<h8*>(Ks + kr * KLD + dd) = v;
+      }
+      for (int e = tid; e < KT * (DV / 8); e += 256) {
+        const int kr = e / (DV / 8), dd = (e - kr * (DV / 8)) * 8;
+        const int key = key0 + kr;
+        h8 v = {};
+        if (key < p.nk) {
+          if (dd + 8 <= p.d) v = *reinterpret_cast<const h8*>(vbase + (size_t)key * p.v_ld + dd);
+          else if (ones_row && dd <= p.d && p.d < dd + 8) v[p.d - dd] = (half_t)1.0f;
+        }
+        *reinterpret_cast<h8*>(Vs + kr * VLD + dd) = v;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < KV_K; ++i) {
+        const int e = tid + 256 * i;
+        const int kr = e / (DQK / 8), dd = (e - kr * (DQK / 8)) * 8;
+        if (e < KT * (DQK / 8)) *reinterpret_cast<h8*>(Ks + kr * KLD + dd) = pk_k[i];
+      }
+#pragma unroll
+      for (int i = 0; i < KV_V; ++i) {
+        const int e = tid + 256 * i;
+        const int kr = e / (DV / 8), dd = (e - kr * (DV / 8)) * 8;
+        if (e < KT * (DV / 8)) *reinterpret_cast<h8*>(Vs + kr * VLD + dd) = pk_v[i];
+      }
     }
     __syncthreads();
+    if (PREFETCH && t + 1 < ntiles) fetch(key0 + KT);
 
     // S^T = K Q^T for two 32-key sub-blocks (raw, unscaled scores)
     f16v s[2];

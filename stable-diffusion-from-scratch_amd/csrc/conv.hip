@@ -384,6 +384,8 @@ __device__ __forceinline__ void epilogue_direct(const Params& p, f16v (&acc)[FM]
   const int lane = threadIdx.x & 63;
   const int fr = lane & 31, fh = lane >> 5;
   const int mode = p.out_mode;
+  // 16-B vector loads of the bias / embedding rows when aligned (channels come in 4s)
+  const bool rb_vec = p.row_bias && !((uintptr_t)p.row_bias & 15) && !(p.rb_ld & 3);
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
     const int m = m0 + m_w + i * 32 + fr;
@@ -410,11 +412,15 @@ __device__ __forceinline__ void epilogue_direct(const Params& p, f16v (&acc)[FM]
           const int nx = n0 + n_w + jp * 64 + 8 * g + 4 * fh;      // x rows; gate rows = nx + 32
           const int no = (n0 + n_w) / 2 + jp * 32 + 8 * g + 4 * fh; // output channel
           if (no >= p.N / 2) continue;
+          f4 bx = {0.f, 0.f, 0.f, 0.f}, bg = {0.f, 0.f, 0.f, 0.f};
+          if (p.bias) {
+            bx = *reinterpret_cast<const f4*>(p.bias + nx);
+            bg = *reinterpret_cast<const f4*>(p.bias + nx + 32);
+          }
           h4 o;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const float bx = p.bias ? p.bias[nx + q] : 0.f, bg = p.bias ? p.bias[nx + 32 + q] : 0.f;
-            const float x = acc[i][2 * jp][4 * g + q] + bx, gt = acc[i][2 * jp + 1][4 * g + q] + bg;
+            const float x = acc[i][2 * jp][4 * g + q] + bx[q], gt = acc[i][2 * jp + 1][4 * g + q] + bg[q];
             o[q] = (half_t)(x * gelu_erf(gt));
           }
           if (p.res) {
@@ -426,24 +432,32 @@ __device__ __forceinline__ void epilogue_direct(const Params& p, f16v (&acc)[FM]
         }
       continue;
     }
+    if (mode == SDK_OUT_NHWC_F16) {
 #pragma unroll
-    for (int j = 0; j < FN; ++j)
+      for (int j = 0; j < FN; ++j)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int n = n0 + n_w + j * 32 + 8 * g + 4 * fh;
-        if (n >= p.N) continue;                         // N % 4 == 0 for the fp16 modes
-        float v[4];
+        for (int g = 0; g < 4; ++g) {
+          const int n = n0 + n_w + j * 32 + 8 * g + 4 * fh;
+          if (n >= p.N) continue;                       // N % 8 == 0 in this mode
+          float v[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = acc[i][j][4 * g + q];
-        if (p.bias) {
+          for (int q = 0; q < 4; ++q) v[q] = acc[i][j][4 * g + q];
+          if (p.bias) {
+            const f4 bb = *reinterpret_cast<const f4*>(p.bias + n);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] += (n + q < p.N) ? p.bias[n + q] : 0.f;
-        }
-        if (p.row_bias) {
+            for (int q = 0; q < 4; ++q) v[q] += bb[q];
+          }
+          if (p.row_bias) {
+            const float* rb = p.row_bias + (size_t)b * p.rb_ld + n;
+            if (rb_vec) {
+              const f4 r4 = *reinterpret_cast<const f4*>(rb);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] += (n + q < p.N) ? p.row_bias[(size_t)b * p.rb_ld + n + q] : 0.f;
-        }
-        if (mode == SDK_OUT_NHWC_F16) {
+              for (int q = 0; q < 4; ++q) v[q] += r4[q];
+            } else {
+#pragma unroll
+              for (int q = 0; q < 4; ++q) v[q] += rb[q];
+            }
+          }
           h4 o;
 #pragma unroll
           for (int q = 0; q < 4; ++q) o[q] = (half_t)v[q];
@@ -453,18 +467,28 @@ __device__ __forceinline__ void epilogue_direct(const Params& p, f16v (&acc)[FM]
             for (int q = 0; q < 4; ++q) o[q] = (half_t)((float)o[q] + (float)rr[q]);
           }
           *reinterpret_cast<h4*>(reinterpret_cast<half_t*>(p.out) + (size_t)m * p.out_ld + n) = o;
-        } else {
-          float* out = reinterpret_cast<float*>(p.out);
+        }
+      continue;
+    }
+    // fp32 outputs (NCHW image, token rows): any N
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            if (n + q >= p.N) continue;
-            float x = v[q];
-            if (p.res) x += (float)p.res[(size_t)m * p.res_ld + n + q];
-            if (mode == SDK_OUT_NCHW_F32)
-              out[((size_t)b * p.N + n + q) * p.hw_out + (m - b * p.hw_out)] = x;
-            else
-              out[(size_t)m * p.out_ld + n + q] = x;
-          }
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n = n0 + n_w + j * 32 + 8 * g + 4 * fh;
+        if (n >= p.N) continue;
+        float* out = reinterpret_cast<float*>(p.out);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (n + q >= p.N) continue;
+          float x = acc[i][j][4 * g + q];
+          if (p.bias) x += p.bias[n + q];
+          if (p.row_bias) x += p.row_bias[(size_t)b * p.rb_ld + n + q];
+          if (p.res) x += (float)p.res[(size_t)m * p.res_ld + n + q];
+          if (mode == SDK_OUT_NCHW_F32)
+            out[((size_t)b * p.N + n + q) * p.hw_out + (m - b * p.hw_out)] = x;
+          else
+            out[(size_t)m * p.out_ld + n + q] = x;
         }
       }
   }

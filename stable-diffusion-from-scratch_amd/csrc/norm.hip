@@ -15,18 +15,24 @@
 namespace sdk {
 namespace {
 
-constexpr int GN_ROWS_PER_THREAD = 32;
+constexpr int GN_U = 8;   // independent 16-B row loads in flight per thread
 
+// Row chunking: a block covers `chunk_rows` pixels of one image; a thread owns 8 channels
+// of every ry-th row in it and keeps GN_U loads in flight; ~1500 blocks per launch so
+// the whole tensor streams at HBM rate instead of a latency-bound 32-row walk.
 struct GnGeom {
   int c8, nv, ry, chunk_rows, nchunks;
 };
 
-GnGeom gn_geom(int hw, int channels) {
+GnGeom gn_geom(int batch, int hw, int channels) {
   GnGeom g;
   g.c8 = channels / 8;
   g.nv = (g.c8 + 255) / 256;
   g.ry = g.nv > 1 ? 1 : std::max(1, 256 / g.c8);
-  g.chunk_rows = g.ry * GN_ROWS_PER_THREAD;
+  const int step = g.ry * GN_U;
+  const int want = std::max(1, (1536 + batch - 1) / std::max(batch, 1));
+  const int per = std::max(1, (hw + want - 1) / want);
+  g.chunk_rows = (per + step - 1) / step * step;
   g.nchunks = (hw + g.chunk_rows - 1) / g.chunk_rows;
   return g;
 }
@@ -53,19 +59,26 @@ __global__ void __launch_bounds__(256) gn_partial_kernel(const half_t* s0, const
     for (int j = 0; j < 8; ++j) { sum[j] = 0.f; sq[j] = 0.f; piv[j] = 0.f; }
     if (active) {
       const int c = vec * 8;
-      h8 pv = load_px(s0, s1, c_split, ld0, ld1, img, c);
+      const h8 pv = load_px(s0, s1, c_split, ld0, ld1, img, c);
 #pragma unroll
       for (int j = 0; j < 8; ++j) piv[j] = (float)pv[j];
       const int rstart = r0 + (g.nv > 1 ? 0 : ysub);
       const int rstep = g.nv > 1 ? 1 : g.ry;
-      for (int r = rstart; r < r1; r += rstep) {
-        h8 v = load_px(s0, s1, c_split, ld0, ld1, img + r, c);
+      for (int r = rstart; r < r1; r += GN_U * rstep) {
+        h8 v[GN_U];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float d = (float)v[j] - piv[j];
-          sum[j] += d;
-          sq[j] += d * d;
+        for (int u = 0; u < GN_U; ++u) {
+          const int rr = r + u * rstep;
+          v[u] = rr < r1 ? load_px(s0, s1, c_split, ld0, ld1, img + rr, c) : pv;   // pivot adds 0
         }
+#pragma unroll
+        for (int u = 0; u < GN_U; ++u)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float d = (float)v[u][j] - piv[j];
+            sum[j] += d;
+            sq[j] += d * d;
+          }
       }
     }
     if (g.ry == 1) {
@@ -94,40 +107,51 @@ __global__ void __launch_bounds__(256) gn_partial_kernel(const half_t* s0, const
   }
 }
 
-// grid (groups, batch), 64 threads (one wave): per channel merge chunks in double,
-// then Chan-merge the group's channels.
-__global__ void __launch_bounds__(64) gn_finalize_kernel(const half_t* s0, const half_t* s1, int c_split, int ld0,
-                                                         int ld1, int hw, int channels, int groups, GnGeom g,
-                                                         const float2* partial, float eps, const float* gamma,
-                                                         const float* beta, float* scale, float* shift) {
-  const int grp = blockIdx.x, b = blockIdx.y, lane = threadIdx.x;
+// grid (groups, batch), 256 threads: wave w merges the chunk partials of channels
+// w, w+4, ... with its 64 lanes striding over chunks (double, shuffle-reduced), then wave
+// 0 Chan-merges the group's channels.
+__device__ __forceinline__ double wave_sum_d(double v) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__global__ void __launch_bounds__(256) gn_finalize_kernel(const half_t* s0, const half_t* s1, int c_split, int ld0,
+                                                          int ld1, int hw, int channels, int groups, GnGeom g,
+                                                          const float2* partial, float eps, const float* gamma,
+                                                          const float* beta, float* scale, float* shift) {
+  __shared__ double cm[256], cq[256];   // per-channel mean, M2 (cg <= 256)
+  const int grp = blockIdx.x, b = blockIdx.y, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int cg = channels / groups, c0 = grp * cg;
   const size_t img = (size_t)b * hw;
-  // each lane owns channels c0+lane, c0+lane+64, ... (cg <= 64*4)
-  double mean_sum = 0.0, m2_sum = 0.0, msq_sum = 0.0;
   const double n = (double)hw;
-  for (int ci = lane; ci < cg; ci += 64) {
+  for (int ci = wave; ci < cg; ci += 4) {
     const int c = c0 + ci;
     double a1 = 0.0, a2 = 0.0;
-    for (int k = 0; k < g.nchunks; ++k) {
+    for (int k = lane; k < g.nchunks; k += 64) {
       const float2 v = partial[((size_t)b * g.nchunks + k) * channels + c];
       a1 += v.x;
       a2 += v.y;
     }
-    // the pivot pass 1 subtracted: this channel's value at pixel 0 of the image
-    const float piv = c < c_split ? (float)s0[img * ld0 + c] : (float)s1[img * ld1 + (c - c_split)];
-    const double mc = (double)piv + a1 / n;
-    const double m2c = a2 - a1 * a1 / n;
-    mean_sum += mc;
-    msq_sum += mc * mc;
-    m2_sum += m2c;
+    a1 = wave_sum_d(a1);
+    a2 = wave_sum_d(a2);
+    if (lane == 0) {
+      // the pivot pass 1 subtracted: this channel's value at pixel 0 of the image
+      const float piv = c < c_split ? (float)s0[img * ld0 + c] : (float)s1[img * ld1 + (c - c_split)];
+      cm[ci] = (double)piv + a1 / n;
+      cq[ci] = a2 - a1 * a1 / n;
+    }
   }
-  // wave reduce
-  for (int off = 32; off > 0; off >>= 1) {
-    mean_sum += __shfl_xor(mean_sum, off, 64);
-    msq_sum += __shfl_xor(msq_sum, off, 64);
-    m2_sum += __shfl_xor(m2_sum, off, 64);
+  __syncthreads();
+  if (wave != 0) return;
+  double mean_sum = 0.0, m2_sum = 0.0, msq_sum = 0.0;
+  for (int ci = lane; ci < cg; ci += 64) {
+    mean_sum += cm[ci];
+    msq_sum += cm[ci] * cm[ci];
+    m2_sum += cq[ci];
   }
+  mean_sum = wave_sum_d(mean_sum);
+  msq_sum = wave_sum_d(msq_sum);
+  m2_sum = wave_sum_d(m2_sum);
   const double mg = mean_sum / cg;
   // sum over channels of n*(mc - mg)^2 = n*(sum mc^2 - cg*mg^2)
   double m2g = m2_sum + n * (msq_sum - cg * mg * mg);
@@ -235,7 +259,7 @@ using namespace sdk;
 
 extern "C" int64_t sdk_group_norm_workspace(int32_t batch, int32_t hw, int32_t channels) {
   if (batch <= 0 || hw <= 0 || channels <= 0) return 0;
-  GnGeom g = gn_geom(hw, channels);
+  GnGeom g = gn_geom(batch, hw, channels);
   return (int64_t)batch * g.nchunks * channels * (int64_t)sizeof(float2);
 }
 
@@ -249,14 +273,14 @@ extern "C" int sdk_group_norm_affine(const sdk_group_norm_args* a, sdk_stream_t 
   if (a->channels / 8 > 512) return fail(SDK_EINVAL, "group_norm: channels > 4096");
   const int64_t need = sdk_group_norm_workspace(a->batch, a->hw, a->channels);
   if (!a->workspace || a->workspace_bytes < need) return fail(SDK_EWORKSPACE, "group_norm: workspace too small");
-  GnGeom g = gn_geom(a->hw, a->channels);
+  GnGeom g = gn_geom(a->batch, a->hw, a->channels);
   hipStream_t s = (hipStream_t)stream;
   const size_t lds = g.ry > 1 ? (size_t)2 * g.ry * g.c8 * 8 * sizeof(float) : 0;
   hipLaunchKernelGGL(gn_partial_kernel, dim3(g.nchunks, a->batch), dim3(256), lds, s, (const half_t*)a->src0,
                      (const half_t*)a->src1, a->c_split, a->ld0, a->ld1, a->hw, a->channels, g,
                      (float2*)a->workspace);
   if (int e = check_launch("gn_partial")) return e;
-  hipLaunchKernelGGL(gn_finalize_kernel, dim3(a->groups, a->batch), dim3(64), 0, s, (const half_t*)a->src0,
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3(a->groups, a->batch), dim3(256), 0, s, (const half_t*)a->src0,
                      (const half_t*)a->src1, a->c_split, a->ld0, a->ld1, a->hw, a->channels, a->groups, g,
                      (const float2*)a->workspace, a->eps, a->gamma, a->beta, a->scale, a->shift);
   return check_launch("gn_finalize");

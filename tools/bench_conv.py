@@ -4,13 +4,17 @@ import ctypes, json, os, subprocess, sys
 import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-SHAPES = [  # (name, B, H, W, Cin, Cout, k, stride, upsample, cin2)
+SHAPES = [  # (name, B, H, W, Cin, Cout, k, stride, upsample, geglu)
     ("unet64_320x320_3x3", 16, 64, 64, 320, 320, 3, 1, False, 0),
     ("unet64_640x320_3x3", 16, 64, 64, 640, 320, 3, 1, False, 0),
     ("unet32_640x640_3x3", 16, 32, 32, 640, 640, 3, 1, False, 0),
     ("unet16_1280x1280_3x3", 16, 16, 16, 1280, 1280, 3, 1, False, 0),
     ("unet8_2560x1280_3x3", 16, 8, 8, 2560, 1280, 3, 1, False, 0),
-    ("unet64_ff1_320x2560", 16, 64, 64, 320, 2560, 1, 1, False, 0),
+    ("unet64_ff1_320x2560", 16, 64, 64, 320, 2560, 1, 1, False, 1),
+    ("unet64_proj_320x320", 16, 64, 64, 320, 320, 1, 1, False, 0),
+    ("unet32_proj_640x640", 16, 32, 32, 640, 640, 1, 1, False, 0),
+    ("unet16_proj_1280x1280", 16, 16, 16, 1280, 1280, 1, 1, False, 0),
+    ("unet32_ff1_640x5120", 16, 32, 32, 640, 5120, 1, 1, False, 1),
     ("unet64_ff2_1280x320", 16, 64, 64, 1280, 320, 1, 1, False, 0),
     ("unet64_qkv_320x960", 16, 64, 64, 320, 960, 1, 1, False, 0),
     ("unet32_up_640x640", 16, 16, 16, 640, 640, 3, 1, True, 0),
@@ -35,11 +39,12 @@ def child():
     sd_amd_loader.load()
     from sd_amd import ops
     res = {}
-    for name, B, H, W, Ci, Co, k, st, up, _ in SHAPES:
+    for name, B, H, W, Ci, Co, k, st, up, geglu in SHAPES:
         x = torch.randn(B, H, W, Ci, device="cuda").half()
         w = torch.randn(Co, Ci, k, k, device="cuda") / (Ci * k * k) ** 0.5
-        pc = ops.PackedConv([(w, Ci)], torch.zeros(Co, device="cuda"), device="cuda")
-        f = lambda: ops.conv2d(pc, x, stride=st, pad=k // 2, upsample=up)
+        pc = ops.PackedConv([(w, Ci)], torch.zeros(Co, device="cuda"), geglu=bool(geglu), device="cuda")
+        mode = ops.OUT_GEGLU_F16 if geglu else ops.OUT_NHWC_F16
+        f = lambda: ops.conv2d(pc, x, stride=st, pad=k // 2, upsample=up, out_mode=mode)
         y = f()
         torch.cuda.synchronize()
         ts = []

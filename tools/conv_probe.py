@@ -16,15 +16,16 @@ def main():
     spec = {s[0]: s[1:] for s in SHAPES}.get(name)
     if spec is None:
         B, H, W, Ci, Co, k, up = (int(v) for v in name.split(","))
-        st = 1
+        st, geglu = 1, 0
     else:
-        B, H, W, Ci, Co, k, st, up, _ = spec
+        B, H, W, Ci, Co, k, st, up, geglu = spec
     torch.manual_seed(0)
     x = torch.randn(B, H, W, Ci, device="cuda").half()
     w = torch.randn(Co, Ci, k, k, device="cuda") / (Ci * k * k) ** 0.5
-    pc = ops.PackedConv([(w, Ci)], torch.zeros(Co, device="cuda"), device="cuda")
+    pc = ops.PackedConv([(w, Ci)], torch.zeros(Co, device="cuda"), geglu=bool(geglu), device="cuda")
     kw = dict(stride=st, pad=k // 2, upsample=bool(up), variant=None if variant < 0 else variant,
-              split_k=None if split <= 0 else split)
+              split_k=None if split <= 0 else split,
+              out_mode=ops.OUT_GEGLU_F16 if geglu else ops.OUT_NHWC_F16)
     y = ops.conv2d(pc, x, **kw)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
