@@ -174,11 +174,10 @@ def main():
     sampler = DDIMSampler(model)
 
     # host-generated global batch, sliced per rank (parity with any rank count)
-    g = torch.Generator().manual_seed(2024)
-    xT_all = torch.randn(world * B, 4, L, L, generator=g)
-    ctx_all = torch.randn(world * B, *cfg["ctx"], generator=g) if cfg["ctx"] else None
-    xT = xT_all[rank * B:(rank + 1) * B].to(device)
-    ctx = ctx_all[rank * B:(rank + 1) * B].to(device) if ctx_all is not None else None
+    from sd_amd import distributed as sdd
+    xT_all, ctx_all = sdd.global_inputs(2024, world, B, (4, L, L), cfg["ctx"])
+    xT = sdd.shard(xT_all, rank, world).to(device)
+    ctx = sdd.shard(ctx_all, rank, world).to(device) if ctx_all is not None else None
     gathered = torch.empty(world * B, 3, 8 * L, 8 * L, dtype=torch.float16, device=device) if dist else None
 
     def one_step():
@@ -186,8 +185,7 @@ def main():
                               verbose=False, log_every_t=10 ** 9)
         img = model.decode_first_stage(z)
         if dist:
-            import torch.distributed as tdist
-            tdist.all_gather_into_tensor(gathered, img.half())
+            sdd.gather(img.half(), world, out=gathered)
         return img
 
     def barrier():
@@ -213,11 +211,7 @@ def main():
         img = one_step()
     barrier()
     elapsed = time.perf_counter() - t0
-    if dist:
-        import torch.distributed as tdist
-        tt = torch.tensor([elapsed], device=device)
-        tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
-        elapsed = tt.item()
+    elapsed = sdd.max_over_ranks(elapsed, device=device)
     finite = bool(torch.isfinite(img).all().item())
 
     # UNet step latency at the config batch (HIP events around replays of the sampler's UNet call)
