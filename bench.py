@@ -139,6 +139,20 @@ def cpu_baseline(cfg_name, cfg, ddim_steps, threads):
                       f"{L}x{L} latent, extrapolated to {ddim_steps} DDIM steps + decode per image"}
 
 
+def pmc_traffic(args):
+    """HBM bytes per conv launch from the committed rocprofv3 PMC passes (FETCH_SIZE / WRITE_SIZE,
+    gfx950-corrected, tools/prof_summary.py) of this same workload — only when they were taken
+    on the current conv kernel source (else null: counters cannot be read from inside the run)."""
+    p = os.path.join(ROOT, "profiles", "conv_traffic.json")
+    if args.config != "c3" or args.ddim_steps != 50 or not os.path.exists(p):
+        return None
+    from sd_amd import ops
+    d = json.load(open(p))
+    if d.get("conv_source") != ops._conv_source_hash() or "traffic_bytes_per_launch" not in d:
+        return None
+    return round(d["traffic_bytes_per_launch"])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -151,6 +165,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-autotune", action="store_true")
+    ap.add_argument("--tuning-cache", default=os.path.join(ROOT, "configs", "conv_tuning_mi355x.json"),
+                    help="conv tile/split-K table measured on MI355X (loaded if present; missing problems are timed)")
+    ap.add_argument("--tuning-out", default=None, help="write the (extended) tuning table here")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one HIP graph per UNet step")
     args = ap.parse_args()
 
@@ -196,10 +213,16 @@ def main():
 
     # the first warm-up step also autotunes every distinct conv problem (tile config x split-K);
     # the UNet graph is captured on its first graphed call, after the eager autotuning call
+    cached = 0
+    if args.tuning_cache and os.path.exists(args.tuning_cache) and not args.no_autotune:
+        cached = ops.AUTOTUNE.load(args.tuning_cache)
     ops.AUTOTUNE.enable(not args.no_autotune)
     model.graph = False
     one_step()
     ops.AUTOTUNE.enable(False)
+    if args.tuning_out and rank == 0 and len(ops.AUTOTUNE.table) > cached:
+        os.makedirs(os.path.dirname(os.path.abspath(args.tuning_out)), exist_ok=True)
+        ops.AUTOTUNE.save(args.tuning_out)
     model.graph = not args.no_graph
     if model.graph:                      # capture the UNet graph (setup, not a sampling step)
         model.apply_model(xT, torch.full((B,), 999, dtype=torch.long, device=device), ctx)
@@ -249,10 +272,10 @@ def main():
                       "latent": [4, L, L], "image": [3, 8 * L, 8 * L], "ddim_steps": args.ddim_steps, "eta": 0.0,
                       "parallelism": f"dp{world}", "collective": "all_gather decoded images (RCCL)" if dist else None},
            "unet_step_ms": round(unet_ms, 3), "finite": finite, "hip_graph": not args.no_graph,
-           "autotuned_conv_problems": len(ops.AUTOTUNE.table)}
+           "autotuned_conv_problems": len(ops.AUTOTUNE.table), "tuning_cache_entries": cached}
     if not args.no_roofline and rank == 0:
         summ = ops.PROFILER.summary()
-        conv = {"launches": 0, "ms": 0.0, "flops": 0.0}
+        conv = {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0}
         for k, d in summ.items():
             if k.startswith("conv"):
                 for f in conv:
@@ -261,10 +284,12 @@ def main():
             avg_s = conv["ms"] / 1000.0 / conv["launches"]
             ach = conv["flops"] / conv["launches"] / avg_s / 1e12
             out["roofline"] = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
-                               "frac": round(ach / PEAK_F16_TFLOPS, 4), "traffic": None,
+                               "frac": round(ach / PEAK_F16_TFLOPS, 4), "traffic": pmc_traffic(args),
                                "kernel": "conv_igemm_kernel (+splitk_reduce_kernel on split-K launches)",
                                "launches": conv["launches"], "avg_launch_us": round(1e6 * avg_s, 2),
-                               "flops_per_launch": conv["flops"] / conv["launches"]}
+                               "flops_per_launch": conv["flops"] / conv["launches"],
+                               "algorithmic_bytes_per_launch": round(conv["bytes"] / conv["launches"]),
+                               "traffic_unit": "bytes per launch (PMC, profiles/conv_traffic.json)"}
         out["kernel_time_ms_profiled_step"] = {k: round(v["ms"], 2) for k, v in summ.items()}
         if os.environ.get("BENCH_SHAPES_OUT"):
             with open(os.environ["BENCH_SHAPES_OUT"], "w") as f:

@@ -157,6 +157,13 @@ class PackedConv:
         self.bias = b.to(device=device, dtype=torch.float32).contiguous() if b is not None else None
 
 
+def _conv_source_hash():
+    import hashlib
+    import os
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc", "conv.hip"), "rb") as f:
+        return hashlib.sha1(f.read()).hexdigest()[:16]
+
+
 class _Autotune:
     """Per-shape choice of conv tile configuration and split-K, measured on the device.
 
@@ -173,10 +180,32 @@ class _Autotune:
     def enable(self, on=True):
         self.enabled = on
 
+    def save(self, path):
+        """Write the table as JSON (key tuple -> [variant_hint, split_k]); a tuning cache
+        like MIOpen's find-db: later runs load it and time nothing."""
+        import json
+        with open(path, "w") as f:
+            json.dump({"device": torch.cuda.get_device_name(0) if torch.cuda.is_available() else None,
+                       "conv_source": _conv_source_hash(),
+                       "entries": [[list(k), list(v)] for k, v in sorted(self.table.items(), key=str)]}, f, indent=0)
+
+    def load(self, path):
+        import json
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("conv_source") != _conv_source_hash():
+            return 0                     # tuned against other kernel code: re-time everything
+        n = 0
+        for k, v in d["entries"]:
+            self.table[tuple(k)] = tuple(v)
+            n += 1
+        return n
+
     def key(self, a, pc):
         s0, s1 = a.seg[0], a.seg[1]
         return (a.batch, a.ho, a.wo, a.cout, a.nseg, pc.k_total, a.out_mode, s0.cin, s0.h, s0.w, s0.ksize,
-                s0.stride, s0.upsample, s0.c_split, bool(s0.gn_scale) or bool(s0.silu), s1.cin if a.nseg > 1 else 0)
+                s0.stride, s0.upsample, s0.c_split, int(bool(s0.gn_scale) or bool(s0.silu)),
+                s1.cin if a.nseg > 1 else 0)
 
     def choose(self, a, pc, dev):
         key = self.key(a, pc)
@@ -276,7 +305,12 @@ def conv2d(pc: PackedConv, x, *, ksize=None, stride=1, pad=None, upsample=False,
         a.workspace = ws.data_ptr()
         a.workspace_bytes = ws.numel()
     if PROFILER.active:
-        PROFILER.begin("conv", info, shape=(B * Ho * Wo, pc.N, pc.k_total, info.variant, info.split_k))
+        # algorithmic HBM bytes: each source tensor, the weights and the output once (+ residual)
+        nb = sum(t.numel() * 2 for t in _as_pair(x) if t is not None) + pc.N * pc.k_total * 2
+        if seg2 is not None:
+            nb += sum(t.numel() * 2 for t in _as_pair(seg2[0]) if t is not None)
+        nb += out.numel() * out.element_size() + (residual.numel() * 2 if residual is not None else 0)
+        PROFILER.begin("conv", info, shape=(B * Ho * Wo, pc.N, pc.k_total, info.variant, info.split_k), nbytes=nb)
     check(lib().sdk_conv2d(C.byref(a), _stream()), "conv2d")
     if PROFILER.active:
         PROFILER.end()
@@ -468,7 +502,7 @@ class _Profiler:
     def stop(self):
         self.active = False
 
-    def begin(self, kind, info, shape=None):
+    def begin(self, kind, info, shape=None, nbytes=0):
         s = torch.cuda.current_stream()
         e0 = torch.cuda.Event(enable_timing=True)
         e0.record(s)
@@ -478,20 +512,20 @@ class _Profiler:
             flops = 4.0 * b * h * nq * nk * d
             shape = info
         variant = info.variant if isinstance(info, ConvPlanInfo) else None
-        self._cur = (kind, variant, flops, e0, shape)
+        self._cur = (kind, variant, flops, e0, shape, nbytes)
 
     def end(self):
         s = torch.cuda.current_stream()
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record(s)
-        kind, variant, flops, e0, shape = self._cur
-        self.records.append((kind, variant, flops, e0, e1, shape))
+        kind, variant, flops, e0, shape, nbytes = self._cur
+        self.records.append((kind, variant, flops, e0, e1, shape, nbytes))
 
     def shape_table(self):
         """Per (kind, shape) totals: launches, ms, TFLOP/s — where the time goes."""
         torch.cuda.synchronize()
         out = {}
-        for kind, variant, flops, e0, e1, shape in self.records:
+        for kind, variant, flops, e0, e1, shape, _ in self.records:
             d = out.setdefault((kind, shape), [0, 0.0, 0.0])
             d[0] += 1
             d[1] += e0.elapsed_time(e1)
@@ -502,10 +536,11 @@ class _Profiler:
     def summary(self):
         torch.cuda.synchronize()
         out = {}
-        for kind, variant, flops, e0, e1, shape in self.records:
+        for kind, variant, flops, e0, e1, shape, nbytes in self.records:
             key = kind if variant is None else f"{kind}:{variant}"
-            d = out.setdefault(key, {"launches": 0, "ms": 0.0, "flops": 0.0})
+            d = out.setdefault(key, {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0})
             d["launches"] += 1
+            d["bytes"] += nbytes
             d["ms"] += e0.elapsed_time(e1)
             d["flops"] += flops or 0.0
         return out
