@@ -36,7 +36,8 @@ class FlashAttentionBlock(nn.Module):
 
     def _run(self, x):
         B, H, W, C = x.shape
-        qkv = ops.conv2d(self._pc_qkv, x, gn=gn_stats(self.norm, x)).view(B * H * W, 3 * C)
+        xn = ops.group_norm_apply(x, gn_stats(self.norm, x), silu=False)
+        qkv = ops.conv2d(self._pc_qkv, xn).view(B * H * W, 3 * C)
         o = ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], batch=B, heads=self.num_heads, nq=H * W,
                           nk=H * W, head_dim=self.head_dim, scale=self.head_dim ** -0.5)
         return ops.conv2d(self._pc_o, o.view(B, H, W, C), residual=x)

@@ -12,6 +12,9 @@ LIB = os.path.join(HERE, "libsdk_amd.so")
 SOURCES = ["conv.hip", "norm.hip", "attention.hip", "sampler.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result"]
+# attention: IEEE mode off + no NaN semantics, so fmaxf on MFMA results is one v_max3 instead of
+# canonicalising v_max x,x copies first (the inputs are finite fp16 products)
+EXTRA = {"attention.hip": ["-mno-amdgpu-ieee", "-fno-honor-nans"]}
 
 
 def _needs(obj: str, deps) -> bool:
@@ -29,7 +32,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         s = os.path.join(CSRC, src)
         o = os.path.join(BUILD, src.replace(".hip", ".o"))
         if force or _needs(o, [s] + headers):
-            jobs.append([HIPCC, *FLAGS, "-c", s, "-o", o])
+            jobs.append([HIPCC, *FLAGS, *EXTRA.get(src, []), "-c", s, "-o", o])
 
     def run(cmd):
         r = subprocess.run(cmd, capture_output=True, text=True)

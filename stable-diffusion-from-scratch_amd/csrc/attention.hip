@@ -1,24 +1,34 @@
 // Flash-style attention forward for gfx950: O = softmax(scale*Q K^T) V, fp16 I/O,
 // fp32 scores/softmax, v_mfma_f32_32x32x16_f16.
 //
-// Workgroup = 4 waves = 128 query rows of one (batch, head); each wave owns 32
-// rows.  Keys stream through LDS in tiles of 64.  The score tile is computed
-// transposed, S^T = K Q^T (A = K rows from LDS, B = Q^T fragments held in
-// registers for the whole loop), so each lane owns ONE query row: the softmax
-// row max / row sum are in-register reductions plus one exchange with lane^32.
-// The S^T accumulator, converted to fp16, is directly the B operand of
-// O^T += V^T P^T (its row index = the key = the contraction index).  V stays
-// row-major in LDS and the V^T operand is read with ds_read_b64_tr_b16 (the
-// hardware transpose read), rows padded so a 32-lane half touches 64 distinct
-// banks.
+// Workgroup = NW waves = 32*NW query rows of one (batch, head); each wave owns 32
+// rows.  Keys stream through a double-buffered LDS ring in tiles of 64 (one
+// barrier per tile).  The score tile is computed transposed, S^T = K Q^T (A = K
+// rows from LDS, B = Q^T fragments held in registers for the whole loop), so each
+// lane owns ONE query row: the row max is an in-register v_max3 chain plus one
+// v_permlane32_swap with the other half-wave.  The S^T accumulator, converted to
+// fp16, is directly the B operand of O^T += V^T P^T (its row index = the key = the
+// contraction index).  V stays row-major in LDS and the V^T operand is read with
+// ds_read_b64_tr_b16 (the hardware transpose read).
 //
-// Per-tile VALU is the budget at small head dims (d = 40: 14 MFMAs per 64-key
-// tile), so: the softmax scale is one FMA feeding v_exp_f32 (scores stay raw),
-// key masking runs only in a ragged last tile, the O rescale is skipped when
-// no lane's running max grew, and when d is below the padded V width the row
-// sum comes out of the PV MFMA itself (a ones column in V's zero padding).
-// Head dims that are not multiples of 16/32 (40, 80, 160 in SD-1) are padded
-// inside LDS/registers only; HBM traffic is the unpadded tensors.
+// At SD's small head dims (d = 40: 14 MFMAs per 64-key tile against 32 exp per
+// lane) the loop is VALU-bound, so everything that is not softmax arithmetic is
+// taken off the vector pipe:
+//  * K/V tiles are register-staged through buffer loads whose hardware range check
+//    supplies the zero rows past nk (no per-element predicates); the per-thread
+//    chunk offsets are computed once, a tile costs one v_add per load; the loads of
+//    tile t+2 are issued after the LDS write of tile t+1 (issue-early / write-late);
+//  * only the ceil(d/8) real 16-B chunks of each row are moved; the LDS padding up
+//    to the MFMA widths is zeroed once, and when d < DV the padding holds a column
+//    of ones so the row sum of P comes out of the PV MFMA (O^T row d);
+//  * Q is pre-scaled by scale*log2(e) and the score MFMA chain is seeded with C = -m
+//    (the running row max), so the accumulator is already the exp2 argument and the
+//    common path is one v_exp_f32 per score; the max is only raised when a row's
+//    tile max exceeds it by more than 8 (defer-max: P <= 256, exact in fp16), so the
+//    rescale of O (and of the scores) is rare;
+//  * key masking runs only in a ragged last tile.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace sdk {
@@ -35,47 +45,110 @@ struct AttnParams {
 };
 
 typedef __fp16 fp16x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u4 __attribute__((ext_vector_type(4)));
 
-constexpr int KT = 64;          // keys per tile
+constexpr int KT = 64;                 // keys per tile
+constexpr float DEFER = 8.0f;          // exp2-domain headroom before the running max is raised
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
-template <int DQK, int DV>
-__global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnParams p) {
+// Buffer descriptor from provably wave-uniform words (readfirstlane of the pointer halves and
+// the size), so hipcc keeps it in SGPRs instead of wrapping every load in a waterfall loop.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long long bytes) {
+  const uint64_t a = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  const int n = __builtin_amdgcn_readfirstlane((int)bytes);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
+}
+
+template <int DQK, int DV, int NW, int QB>
+__global__ void __launch_bounds__(NW * 64, QB == 2 ? 1 : 2) attn_fwd_kernel(AttnParams p) {
+  constexpr int NT = NW * 64;
   constexpr int KLD = DQK + 8;                                       // K row stride (halfs)
   constexpr int VLD = ((DV * 2 / 64) % 2 == 0) ? DV + 32 : DV;       // V row stride: 64 or 192 B mod 256
-  __shared__ __attribute__((aligned(16))) half_t smem[KT * KLD + KT * VLD];
-  half_t* Ks = smem;
-  half_t* Vs = smem + KT * KLD;
+  constexpr int KS = KT * KLD, STAGE = KS + KT * VLD;
+  constexpr int SL = (KT * (DQK / 8) + NT - 1) / NT;                 // staging slots per thread (K and V each)
+  __shared__ __attribute__((aligned(16))) half_t smem[2 * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 31, fh = lane >> 5;
   const int head = blockIdx.y, b = blockIdx.z;
-  const int q0 = blockIdx.x * 128 + wave * 32;
-  const int qrow = q0 + fr;
-  const bool qvalid = qrow < p.nq;
-  const bool ones_row = p.d < DV;          // row sum from the PV MFMA (ones column at d)
+  const int q0 = blockIdx.x * (32 * QB * NW) + wave * 32 * QB;      // this wave's first query row
+  const int d = p.d, nch = (d + 7) >> 3;   // real 16-B chunks per row
+  const bool ones_row = d < DV;            // row sum from the PV MFMA (ones column at d)
 
-  // Q^T fragments (B operand): lane holds Q[qrow][ks*16 + 8*fh + j]
-  h8 qf[DQK / 16];
-  {
-    const half_t* qp = p.q + ((size_t)b * p.nq + (qvalid ? qrow : 0)) * p.q_ld + head * p.d;
+  // zero the LDS padding of both stages once (K columns >= 8*nch, V columns >= 8*nch),
+  // with the ones column at d; the staged chunks never touch it
+  for (int e = tid; e < 2 * KT; e += NT) {
+    half_t* kr = smem + (e / KT) * STAGE + (e % KT) * KLD;
+    for (int c = nch * 8; c < KLD; ++c) kr[c] = (half_t)0.0f;
+    half_t* vr = smem + (e / KT) * STAGE + KS + (e % KT) * VLD;
+    for (int c = nch * 8; c < VLD; ++c) vr[c] = (half_t)((ones_row && c == d) ? 1.0f : 0.0f);
+  }
+
+  // staging slots: chunk e = tid + NT*i of the tile = (key e/nch, chunk e%nch) of K and of V
+  const __amdgpu_buffer_rsrc_t rk = rsrc(p.k + (size_t)b * p.nk * p.k_ld, (long long)p.nk * p.k_ld * 2);
+  const __amdgpu_buffer_rsrc_t rv = rsrc(p.v + (size_t)b * p.nk * p.v_ld, (long long)p.nk * p.v_ld * 2);
+  unsigned gk[SL], gv[SL];
+  int lk[SL], lv[SL];
+#pragma unroll
+  for (int i = 0; i < SL; ++i) {
+    const int e = tid + NT * i;
+    const int key = e / nch, c = e - key * nch;
+    const bool ok = e < KT * nch;
+    gk[i] = (unsigned)((key * p.k_ld + head * d + c * 8) * 2);
+    gv[i] = (unsigned)((key * p.v_ld + head * d + c * 8) * 2);
+    lk[i] = ok ? key * KLD + c * 8 : -1;
+    lv[i] = KS + key * VLD + c * 8;
+  }
+  const unsigned kstep = (unsigned)(KT * p.k_ld * 2), vstep = (unsigned)(KT * p.v_ld * 2);
+  u4 rk_[SL], rv_[SL];
+  auto fetch = [&](int t) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < SL; ++i)
+      if (lk[i] >= 0) {
+        rk_[i] = __builtin_amdgcn_raw_buffer_load_b128(rk, gk[i] + t * kstep, 0, 0);
+        rv_[i] = __builtin_amdgcn_raw_buffer_load_b128(rv, gv[i] + t * vstep, 0, 0);
+      }
+  };
+  auto stage = [&](int buf) __attribute__((always_inline)) {
+    half_t* st = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < SL; ++i)
+      if (lk[i] >= 0) {
+        *reinterpret_cast<u4*>(st + lk[i]) = rk_[i];
+        *reinterpret_cast<u4*>(st + lv[i]) = rv_[i];
+      }
+  };
+
+  // Q^T fragments (B operand) of each 32-row block: lane holds c*Q[row][ks*16 + 8*fh + j]
+  h8 qf[QB][DQK / 16];
+#pragma unroll
+  for (int qb = 0; qb < QB; ++qb) {
+    const int row = q0 + qb * 32 + fr;
+    const half_t* qp = p.q + ((size_t)b * p.nq + (row < p.nq ? row : 0)) * p.q_ld + head * d;
 #pragma unroll
     for (int ks = 0; ks < DQK / 16; ++ks) {
       const int dd = ks * 16 + 8 * fh;
       h8 v = {};
-      if (qvalid && dd < p.d) v = *reinterpret_cast<const h8*>(qp + dd);
-      qf[ks] = v;
+      if (row < p.nq && dd < d) v = *reinterpret_cast<const h8*>(qp + dd);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (half_t)((float)v[j] * p.c);   // scores land in the exp2 domain
+      qf[qb][ks] = v;
     }
   }
 
-  f16v o[DV / 32];
+  f16v o[QB][DV / 32];
 #pragma unroll
-  for (int i = 0; i < DV / 32; ++i) o[i] = f16v{};
-  float m_run = -1e30f, l_run = 0.f;
-
-  const half_t* kbase = p.k + (size_t)b * p.nk * p.k_ld + head * p.d;
-  const half_t* vbase = p.v + (size_t)b * p.nk * p.v_ld + head * p.d;
+  for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+    for (int i = 0; i < DV / 32; ++i) o[qb][i] = f16v{};
+  // running max m (exp2 domain, per query row = per lane); the score chain is seeded with
+  // C = -m, so the MFMA emits s' = c*s - m and the common path is a bare v_exp per score
+  float m_run[QB], l_run[QB];
+  f16v negm[QB];
+#pragma unroll
+  for (int qb = 0; qb < QB; ++qb) { m_run[qb] = 0.f; l_run[qb] = 0.f; negm[qb] = f16v{}; }
   const int ntiles = (p.nk + KT - 1) / KT;
 
   // transposed-read addressing for the V^T operand (32x32x16, A side):
@@ -85,180 +158,151 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnParams p) {
   const int vrow_off = 4 * (g >> 1) + q4;
   const int vcol_off = 16 * (g & 1) + 4 * pp;
 
-  // K/V tiles are prefetched into registers one tile ahead (issue-early / write-late):
-  // the global loads of tile t+1 are in flight while tile t is multiplied
-  constexpr int KV_K = (KT * (DQK / 8) + 255) / 256, KV_V = (KT * (DV / 8) + 255) / 256;
-  h8 pk_k[KV_K], pk_v[KV_V];
-  auto fetch = [&](int key0) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < KV_K; ++i) {
-      const int e = tid + 256 * i;
-      const int kr = e / (DQK / 8), dd = (e - kr * (DQK / 8)) * 8;
-      const int key = key0 + kr;
-      h8 v = {};
-      if (e < KT * (DQK / 8) && key < p.nk && dd < p.d) v = *reinterpret_cast<const h8*>(kbase + (size_t)key * p.k_ld + dd);
-      pk_k[i] = v;
-    }
-#pragma unroll
-    for (int i = 0; i < KV_V; ++i) {
-      const int e = tid + 256 * i;
-      const int kr = e / (DV / 8), dd = (e - kr * (DV / 8)) * 8;
-      const int key = key0 + kr;
-      h8 v = {};
-      if (e < KT * (DV / 8) && key < p.nk) {
-        if (dd + 8 <= p.d) {
-          v = *reinterpret_cast<const h8*>(vbase + (size_t)key * p.v_ld + dd);
-        } else if (ones_row && dd <= p.d && p.d < dd + 8) {
-          v[p.d - dd] = (half_t)1.0f;       // ones column -> row sum of P in O^T row d
-        }
-      }
-      pk_v[i] = v;
-    }
-  };
-  constexpr bool PREFETCH = DV <= 128;   // d = 160 has no registers to spare
-  if (PREFETCH) fetch(0);
-  for (int t = 0; t < ntiles; ++t) {
-    const int key0 = t * KT;
-    __syncthreads();   // previous tile fully consumed
-    if (!PREFETCH) {
-      for (int e = tid; e < KT * (DQK / 8); e += 256) {
-        const int kr = e / (DQK / 8), dd = (e - kr * (DQK / 8)) * 8;
-        const int key = key0 + kr;
-        h8 v = {};
-        if (key < p.nk && dd < p.d) v = *reinterpret_cast<const h8*>(kbase + (size_t)key * p.k_ld + dd);
-        *reinterpret_cast<h8*>(Ks + kr * KLD + dd) = v;
-      }
-      for (int e = tid; e < KT * (DV / 8); e += 256) {
-        const int kr = e / (DV / 8), dd = (e - kr * (DV / 8)) * 8;
-        const int key = key0 + kr;
-        h8 v = {};
-        if (key < p.nk) {
-          if (dd + 8 <= p.d) v = *reinterpret_cast<const h8*>(vbase + (size_t)key * p.v_ld + dd);
-          else if (ones_row && dd <= p.d && p.d < dd + 8) v[p.d - dd] = (half_t)1.0f;
-        }
-        *reinterpret_cast<h8*>(Vs + kr * VLD + dd) = v;
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < KV_K; ++i) {
-        const int e = tid + 256 * i;
-        const int kr = e / (DQK / 8), dd = (e - kr * (DQK / 8)) * 8;
-        if (e < KT * (DQK / 8)) *reinterpret_cast<h8*>(Ks + kr * KLD + dd) = pk_k[i];
-      }
-#pragma unroll
-      for (int i = 0; i < KV_V; ++i) {
-        const int e = tid + 256 * i;
-        const int kr = e / (DV / 8), dd = (e - kr * (DV / 8)) * 8;
-        if (e < KT * (DV / 8)) *reinterpret_cast<h8*>(Vs + kr * VLD + dd) = pk_v[i];
-      }
-    }
-    __syncthreads();
-    if (PREFETCH && t + 1 < ntiles) fetch(key0 + KT);
+  fetch(0);
+  stage(0);
+  if (ntiles > 1) fetch(1);
+  __syncthreads();
 
-    // S^T = K Q^T for two 32-key sub-blocks (raw, unscaled scores)
-    f16v s[2];
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    const half_t* Ks = smem + cur * STAGE;
+    const half_t* Vs = Ks + KS;
+    const int key0 = t * KT;
+
+    // S'^T = K (cQ)^T - m for two 32-key sub-blocks of every query block; each K fragment
+    // is read once for all QB blocks
+    f16v s[QB][2];
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      s[kb] = f16v{};
+    for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
       for (int ks = 0; ks < DQK / 16; ++ks) {
         const h8 a = *reinterpret_cast<const h8*>(Ks + (kb * 32 + fr) * KLD + ks * 16 + 8 * fh);
-        s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, qf[ks], s[kb], 0, 0, 0);
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb)
+          s[qb][kb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, qf[qb][ks], ks == 0 ? negm[qb] : s[qb][kb], 0, 0, 0);
       }
+    // tile t+1 (in registers since last iteration) -> the other stage; then issue t+2
+    if (t + 1 < ntiles) {
+      stage(cur ^ 1);
+      if (t + 2 < ntiles) fetch(t + 2);
     }
-    if (key0 + KT > p.nk) {           // ragged last tile only
+
+    h8 pf[QB][4];
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb) {
+      if (key0 + KT > p.nk) {           // ragged last tile only
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+            if (key >= p.nk) s[qb][kb][r] = -1e30f;
+          }
+      }
+      float mt = fmaxf(s[qb][0][0], s[qb][0][1]);
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
-          if (key >= p.nk) s[kb][r] = -1e30f;
-        }
-    }
-    float mt = s[0][0];
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[kb][r]);
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-    const float m_new = fmaxf(m_run, mt);
-    if (__any(m_new > m_run)) {       // rescale only when some row's max grew
-      const float alpha = fast_exp2((m_run - m_new) * p.c);
-      l_run *= alpha;
-#pragma unroll
-      for (int db = 0; db < DV / 32; ++db)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) o[db][r] *= alpha;
-      m_run = m_new;
-    }
-    const float nmc = -m_run * p.c;
-    h8 pf[4];
-    float ls = 0.f;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int hlf = 0; hlf < 2; ++hlf) {
-        h8 pk;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float e = fast_exp2(fmaf(s[kb][hlf * 8 + j], p.c, nmc));
-          if (!ones_row) ls += e;
-          pk[j] = (half_t)e;
-        }
-        pf[kb * 2 + hlf] = pk;
+        for (int r = (kb == 0 ? 2 : 0); r < 16; r += 2) mt = fmaxf(fmaxf(mt, s[qb][kb][r]), s[qb][kb][r + 1]);
+      {
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mt), __float_as_uint(mt), false, false);
+        mt = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
       }
-    if (!ones_row) l_run += ls + __shfl_xor(ls, 32, 64);
+      // raise the running max only on the first tile or past the headroom (P <= 2^DEFER)
+      if (t == 0 || __any(mt > DEFER)) {
+        const float dm = t == 0 ? mt : fmaxf(mt, 0.f);
+        const float alpha = fast_exp2(-dm);
+        l_run[qb] *= alpha;
+#pragma unroll
+        for (int db = 0; db < DV / 32; ++db)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[qb][db][r] *= alpha;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) s[qb][kb][r] -= dm;
+        m_run[qb] += dm;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) negm[qb][r] = -m_run[qb];
+      }
+      float ls = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int hlf = 0; hlf < 2; ++hlf) {
+          h8 pk;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float e = fast_exp2(s[qb][kb][hlf * 8 + j]);
+            if (!ones_row) ls += e;
+            pk[j] = (half_t)e;
+          }
+          pf[qb][kb * 2 + hlf] = pk;
+        }
+      if (!ones_row) {
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(ls), __float_as_uint(ls), false, false);
+        l_run[qb] += __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+      }
+    }
 
-    // O^T += V^T P^T ; element j of lane half fh in k-step ks is key 16ks + 8(j>>2) + 4fh + (j&3)
+    // O^T += V^T P^T ; element j of lane half fh in k-step ks is key 16ks + 8(j>>2) + 4fh + (j&3);
+    // each V^T fragment (ds_read_b64_tr_b16 pair) is read once for all QB blocks
 #pragma unroll
     for (int db = 0; db < DV / 32; ++db) {
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         const half_t* base = Vs + (16 * ks + vrow_off) * VLD + 32 * db + vcol_off;
-        const fp16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4f16(
-            (__attribute__((address_space(3))) fp16x4_t*)(base));
-        const fp16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4f16(
-            (__attribute__((address_space(3))) fp16x4_t*)(base + 8 * VLD));
+        const fp16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) fp16x4_t*)(base));
+        const fp16x4_t hi =
+            __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) fp16x4_t*)(base + 8 * VLD));
         const h4 lo4 = __builtin_bit_cast(h4, lo), hi4 = __builtin_bit_cast(h4, hi);
         const h8 a = __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7);
-        o[db] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, pf[ks], o[db], 0, 0, 0);
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) o[qb][db] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, pf[qb][ks], o[qb][db], 0, 0, 0);
       }
     }
+    __syncthreads();   // stage `cur` fully read before it is restaged; stage cur^1 visible
   }
 
-  // row sum: explicit, or O^T row d (block d/32, row rho = d%32 held by lanes with h = (rho>>2)&1)
-  float l = l_run;
-  if (ones_row) {
-    const int rho = p.d & 31, hsrc = (rho >> 2) & 1, rsel = (rho & 3) + 4 * (rho >> 3);
-    float v = 0.f;
 #pragma unroll
-    for (int db = 0; db < DV / 32; ++db)
+  for (int qb = 0; qb < QB; ++qb) {
+    // row sum: explicit, or O^T row d (block d/32, row rho = d%32 held by lanes with h = (rho>>2)&1)
+    float l = l_run[qb];
+    if (ones_row) {
+      const int rho = d & 31, hsrc = (rho >> 2) & 1, rsel = (rho & 3) + 4 * (rho >> 3);
+      float v = 0.f;
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        if (db == (p.d >> 5) && r == rsel) v = o[db][r];
-    l = __shfl(v, fr + 32 * hsrc, 64);
-  }
-  if (!qvalid) return;
-  const float inv = 1.f / l;
-  half_t* op = p.o + ((size_t)b * p.nq + qrow) * p.o_ld + head * p.d;
+      for (int db = 0; db < DV / 32; ++db)
 #pragma unroll
-  for (int db = 0; db < DV / 32; ++db)
-#pragma unroll
-    for (int gg = 0; gg < 4; ++gg) {
-      const int dd = db * 32 + 8 * gg + 4 * fh;
-      if (dd < p.d) {
-        h4 w;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) w[j] = (half_t)(o[db][4 * gg + j] * inv);
-        *reinterpret_cast<h4*>(op + dd) = w;
-      }
+        for (int r = 0; r < 16; ++r)
+          if (db == (d >> 5) && r == rsel) v = o[qb][db][r];
+      l = __shfl(v, fr + 32 * hsrc, 64);
     }
+    const int row = q0 + qb * 32 + fr;
+    if (row < p.nq) {
+      const float inv = 1.f / l;
+      half_t* op = p.o + ((size_t)b * p.nq + row) * p.o_ld + head * d;
+#pragma unroll
+      for (int db = 0; db < DV / 32; ++db)
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg) {
+          const int dd = db * 32 + 8 * gg + 4 * fh;
+          if (dd < d) {
+            h4 w;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) w[j] = (half_t)(o[qb][db][4 * gg + j] * inv);
+            *reinterpret_cast<h4*>(op + dd) = w;
+          }
+        }
+    }
+  }
 }
 
-template <int DQK, int DV>
+template <int DQK, int DV, int NW, int QB>
 int launch(const AttnParams& p, hipStream_t s) {
-  dim3 grid((p.nq + 127) / 128, p.heads, p.batch);
-  hipLaunchKernelGGL((attn_fwd_kernel<DQK, DV>), grid, dim3(256), 0, s, p);
+  constexpr int ROWS = 32 * QB * NW;
+  dim3 grid((p.nq + ROWS - 1) / ROWS, p.heads, p.batch);
+  hipLaunchKernelGGL((attn_fwd_kernel<DQK, DV, NW, QB>), grid, dim3(NW * 64), 0, s, p);
   return check_launch("attn_fwd");
 }
 
@@ -274,17 +318,29 @@ extern "C" int sdk_attention(const sdk_attention_args* a, sdk_stream_t stream) {
   if (a->q_ld % 8 || a->k_ld % 8 || a->v_ld % 8 || a->o_ld % 4)
     return fail(SDK_EINVAL, "attention: row strides must be multiples of 8 (o: 4)");
   if (a->nk <= 0 || a->nq <= 0 || a->batch <= 0 || a->heads <= 0) return fail(SDK_EINVAL, "attention: empty");
+  if (a->heads * a->head_dim > a->k_ld || a->heads * a->head_dim > a->v_ld || a->heads * a->head_dim > a->q_ld)
+    return fail(SDK_EINVAL, "attention: row stride smaller than heads*head_dim");
+  if ((double)a->nk * std::max(a->k_ld, a->v_ld) * 2 >= 2147483647.0)
+    return fail(SDK_EINVAL, "attention: one image's K/V exceeds the 2 GiB buffer range");
   AttnParams p{(const half_t*)a->q, (const half_t*)a->k, (const half_t*)a->v, (half_t*)a->o,
                a->q_ld, a->k_ld, a->v_ld, a->o_ld, a->batch, a->heads, a->nq, a->nk, a->head_dim,
                a->scale * 1.4426950408889634f};
   hipStream_t s = (hipStream_t)stream;
   const int d = a->head_dim;
-  if (d <= 16) return launch<16, 32>(p, s);
-  if (d <= 32) return launch<32, 32>(p, s);
-  if (d <= 48) return launch<48, 64>(p, s);
-  if (d <= 64) return launch<64, 64>(p, s);
-  if (d <= 80) return launch<80, 96>(p, s);
-  if (d <= 96) return launch<96, 96>(p, s);
-  if (d <= 128) return launch<128, 128>(p, s);
-  return launch<160, 160>(p, s);
+  // one 32-row query block per wave at 3-4 waves per SIMD; SDK_ATTN_QB=2 selects two blocks per
+  // wave at one wave per SIMD (shared K/V fragments; measured 1.6x slower at d = 40 under hipcc's
+  // scheduling, kept as a tuning knob)
+  static const int qb2 = getenv("SDK_ATTN_QB") && atoi(getenv("SDK_ATTN_QB")) == 2;
+  if (d <= 16) return launch<16, 32, 4, 1>(p, s);
+  if (d <= 32) return launch<32, 32, 4, 1>(p, s);
+  // d <= 80: 8-wave workgroups (half the staging registers: d = 40 127 VGPRs = 4 waves per SIMD,
+  // 547 vs 623 us for the 4-wave form at SD-1's 64x64 level); SDK_ATTN_NW=4 selects the latter.
+  // d = 160 keeps 4 waves: at 256 query rows one 8-wave group per head would idle half the CUs
+  static const int nw4 = getenv("SDK_ATTN_NW") && atoi(getenv("SDK_ATTN_NW")) == 4;
+  if (d <= 48) return qb2 ? launch<48, 64, 4, 2>(p, s) : nw4 ? launch<48, 64, 4, 1>(p, s) : launch<48, 64, 8, 1>(p, s);
+  if (d <= 64) return nw4 ? launch<64, 64, 4, 1>(p, s) : launch<64, 64, 8, 1>(p, s);
+  if (d <= 80) return nw4 ? launch<80, 96, 4, 1>(p, s) : launch<80, 96, 8, 1>(p, s);   // 165 vs 189 VGPRs
+  if (d <= 96) return launch<96, 96, 4, 1>(p, s);
+  if (d <= 128) return launch<128, 128, 4, 1>(p, s);
+  return launch<160, 160, 4, 1>(p, s);
 }

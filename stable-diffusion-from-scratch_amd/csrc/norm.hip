@@ -107,9 +107,10 @@ __global__ void __launch_bounds__(256) gn_partial_kernel(const half_t* s0, const
   }
 }
 
-// grid (groups, batch), 256 threads: wave w merges the chunk partials of channels
-// w, w+4, ... with its 64 lanes striding over chunks (double, shuffle-reduced), then wave
-// 0 Chan-merges the group's channels.
+// grid (groups, batch), 256 threads: the cg channels of the group get tpc = 256/cg (power of
+// two, <= 64) consecutive lanes each; a channel's lanes sum disjoint chunk subsets (all loads
+// independent, so they stream instead of one dependent round trip per channel), reduce with
+// xor shuffles in double, then wave 0 Chan-merges the group's channels.
 __device__ __forceinline__ double wave_sum_d(double v) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
   return v;
@@ -120,25 +121,35 @@ __global__ void __launch_bounds__(256) gn_finalize_kernel(const half_t* s0, cons
                                                           const float2* partial, float eps, const float* gamma,
                                                           const float* beta, float* scale, float* shift) {
   __shared__ double cm[256], cq[256];   // per-channel mean, M2 (cg <= 256)
-  const int grp = blockIdx.x, b = blockIdx.y, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int grp = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int cg = channels / groups, c0 = grp * cg;
   const size_t img = (size_t)b * hw;
   const double n = (double)hw;
-  for (int ci = wave; ci < cg; ci += 4) {
-    const int c = c0 + ci;
+  int tpc = 64;
+  while (tpc > 1 && tpc * cg > 256) tpc >>= 1;
+  const int ci = tid / tpc, sub = tid - ci * tpc;
+  for (int cbase = 0; cbase < cg; cbase += 256 / tpc) {
+    const int cc = cbase + ci;
+    const bool act = ci < 256 / tpc && cc < cg;
     double a1 = 0.0, a2 = 0.0;
-    for (int k = lane; k < g.nchunks; k += 64) {
-      const float2 v = partial[((size_t)b * g.nchunks + k) * channels + c];
-      a1 += v.x;
-      a2 += v.y;
+    if (act) {
+      const float2* pp = partial + (size_t)b * g.nchunks * channels + c0 + cc;
+      for (int k = sub; k < g.nchunks; k += tpc) {
+        const float2 v = pp[(size_t)k * channels];
+        a1 += v.x;
+        a2 += v.y;
+      }
     }
-    a1 = wave_sum_d(a1);
-    a2 = wave_sum_d(a2);
-    if (lane == 0) {
+    for (int off = tpc >> 1; off > 0; off >>= 1) {   // lanes of one channel are contiguous and aligned
+      a1 += __shfl_xor(a1, off, 64);
+      a2 += __shfl_xor(a2, off, 64);
+    }
+    if (act && sub == 0) {
+      const int c = c0 + cc;
       // the pivot pass 1 subtracted: this channel's value at pixel 0 of the image
       const float piv = c < c_split ? (float)s0[img * ld0 + c] : (float)s1[img * ld1 + (c - c_split)];
-      cm[ci] = (double)piv + a1 / n;
-      cq[ci] = a2 - a1 * a1 / n;
+      cm[cc] = (double)piv + a1 / n;
+      cq[cc] = a2 - a1 * a1 / n;
     }
   }
   __syncthreads();

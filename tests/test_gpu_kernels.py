@@ -181,6 +181,28 @@ def test_attention(ops, B, H, nq, nk, d):
     assert rel_l2(o, ref) < 3e-3
 
 
+@pytest.mark.parametrize("B,H,n,nk,d,packed", [
+    (2, 8, 333, 333, 40, "qkv"), (2, 8, 256, 77, 40, "kv"), (1, 8, 1024, 1024, 80, "qkv"), (1, 5, 100, 77, 64, "kv"),
+    (1, 8, 64, 64, 160, "qkv"), (1, 8, 40, 77, 160, "kv"),
+])
+def test_attention_strided_packed(ops, B, H, n, nk, d, packed):
+    """The model's layouts: q|k|v column slices of one projection output (self-attention,
+    row stride 3*H*d), or a k|v pair from the cached context projection (cross-attention)."""
+    from oracle.unet_ref import attention_core
+    C = H * d
+    if packed == "qkv":
+        qkv = _rand(B * n, 3 * C, seed=21).to(DEV)
+        q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
+    else:
+        q = _rand(B * n, C, seed=22).to(DEV)
+        kv = _rand(B * nk, 2 * C, seed=23).to(DEV)
+        k, v = kv[:, :C], kv[:, C:]
+    o = ops.attention(q, k, v, batch=B, heads=H, nq=n, nk=nk, head_dim=d, scale=d ** -0.5)
+    ref = attention_core(q.cpu().float().contiguous().view(B, n, H, d), k.cpu().float().contiguous().view(B, nk, H, d),
+                         v.cpu().float().contiguous().view(B, nk, H, d), d ** -0.5).reshape(B * n, C)
+    assert rel_l2(o, ref) < 3e-3
+
+
 def test_attention_large_logits_rescale(ops):
     """Force the online-softmax max to jump in a late key tile (rule: test the rescale branch)."""
     from oracle.unet_ref import attention_core

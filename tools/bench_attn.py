@@ -14,7 +14,11 @@ SHAPES = [  # name, B, heads, nq, nk, d
     ("sd2_self_96x96_d64", 8, 5, 9216, 9216, 64),
     ("vae_mid_64x64_d64", 16, 8, 4096, 4096, 64),
 ]
+ONLY = sys.argv[1:]          # optional shape-name filter (profiling one kernel)
+REPS = int(os.environ.get("BENCH_REPS", "5"))
 for name, B, H, nq, nk, d in SHAPES:
+    if ONLY and name not in ONLY:
+        continue
     q = torch.randn(B * nq, H * d, device="cuda").half()
     k = torch.randn(B * nk, H * d, device="cuda").half()
     v = torch.randn(B * nk, H * d, device="cuda").half()
@@ -22,7 +26,7 @@ for name, B, H, nq, nk, d in SHAPES:
     f()
     torch.cuda.synchronize()
     ts = []
-    for _ in range(5):
+    for _ in range(REPS):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(5):
@@ -30,7 +34,7 @@ for name, B, H, nq, nk, d in SHAPES:
         e1.record()
         torch.cuda.synchronize()
         ts.append(e0.elapsed_time(e1) / 5)
-    ms = sorted(ts)[2]
+    ms = sorted(ts)[len(ts) // 2]
     fl = 4.0 * B * H * nq * nk * d
     byt = 2.0 * (B * nq * H * d * 2 + 2 * B * nk * H * d)
     print(f"{name:24s} {ms*1000:9.1f} us  {fl/ms/1e9:8.1f} TFLOP/s  {byt/ms/1e6:8.1f} GB/s")
