@@ -291,6 +291,21 @@ def main():
                                "algorithmic_bytes_per_launch": round(conv["bytes"] / conv["launches"]),
                                "traffic_unit": "bytes per launch (PMC, profiles/conv_traffic.json)"}
         out["kernel_time_ms_profiled_step"] = {k: round(v["ms"], 2) for k, v in summ.items()}
+        if os.environ.get("BENCH_SEQ_OUT"):
+            # launch sequence of ONE UNet forward (kind, shape, flops) for tools/trace_step.py,
+            # which pairs it with a graph-replayed step of a rocprofv3 trace (device times)
+            recs = ops.PROFILER.records
+            ops.PROFILER.start()
+            model.graph = False
+            model.apply_model(xT, tts, ctx)
+            torch.cuda.synchronize()
+            ops.PROFILER.stop()
+            model.graph = not args.no_graph
+            seq = [[k, v, fl, list(sh) if isinstance(sh, tuple) else sh]
+                   for k, v, fl, _, _, sh, _ in ops.PROFILER.records]
+            ops.PROFILER.records = recs
+            with open(os.environ["BENCH_SEQ_OUT"], "w") as f:
+                json.dump(seq, f)
         if os.environ.get("BENCH_SHAPES_OUT"):
             with open(os.environ["BENCH_SHAPES_OUT"], "w") as f:
                 for (kind, shape), n, ms, tf in ops.PROFILER.shape_table():

@@ -628,9 +628,10 @@ __device__ __forceinline__ void epilogue_lds(const Params& p, f16v (&acc)[FM][FN
 // applied by gn_apply before 3x3 convs); every segment must be transform-free.
 __device__ __attribute__((aligned(16))) half_t g_zero_page[8];
 
-template <int BM_, int BN_, int WM_, int WN_>
+template <int BM_, int BN_, int WM_, int WN_, int NS_ = 2>
 struct Cfg {
   static constexpr int TBM = BM_, TBN = BN_, WM = WM_, WN = WN_;
+  static constexpr int NS = NS_;                         // LDS ring stages (NS - 1 K-steps of DMA in flight)
   static constexpr int NW = WM * WN, NT = NW * 64;
   static constexpr int TM = TBM / WM, TN = TBN / WN;
   static constexpr int FM = TM / 32, FN = TN / 32;
@@ -640,8 +641,8 @@ struct Cfg {
   static constexpr int GPW = (NINSTR + NW - 1) / NW;     // pieces per wave (padded: the same count in
                                                          // every wave keeps the vmcnt immediate exact)
   static_assert(TBM % 8 == 0 && TBN % 8 == 0, "A/B boundary must align to an 8-row piece");
-  static constexpr int LDS_BYTES = 2 * STAGE_H * 2 + (GPW * NW > NINSTR ? 1024 : 0);  // + dummy slot
-  static_assert(LDS_BYTES <= 160 * 1024, "two stages must fit the 160 KiB LDS");
+  static constexpr int LDS_BYTES = NS * STAGE_H * 2 + (GPW * NW > NINSTR ? 1024 : 0);  // + dummy slot
+  static_assert(LDS_BYTES <= 160 * 1024, "the ring must fit the 160 KiB LDS");
   static_assert(LDS_BYTES / NW >= EPI_BYTES, "per-wave epilogue scratch");
 };
 
@@ -803,13 +804,18 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_glds_kernel(Params p)
   }
   int sg, ky, kx, cb;
   ph_kstate(p, kt0, sg, ky, kx, cb);
+  // K-steps past kt1 still issue their pieces (zero-page DMAs into the idle stage) so every
+  // iteration waits with the same vmcnt immediate
 #define SDK_STAGE(KT_, BUF_)                                                                 \
   do {                                                                                       \
+    const bool live_ = (KT_) < kt1;                                                          \
     _Pragma("unroll") for (int j = 0; j < GPW; ++j) {                                        \
       const int piece = j * CF::NW + wave;                                                   \
       const int rch = (lane & 7) ^ ((4 * piece + (lrow >> 1)) & 7);                          \
       if (piece >= CF::NINSTR) {                                                             \
-        ph_dma(d.w, lds + 2 * CF::STAGE_H, PH_OOB, 0);                                       \
+        ph_dma(d.w, lds + CF::NS * CF::STAGE_H, PH_OOB, 0);                                  \
+      } else if (!live_) {                                                                   \
+        ph_dma(d.w, lds + (BUF_) * CF::STAGE_H + piece * 8 * BK, PH_OOB, 0);                 \
       } else if (piece * 8 < CF::TBM) {                                                      \
         dma_a_piece(p, d, lds + (BUF_) * CF::STAGE_H + piece * 8 * BK, cx[j], cy[j],         \
                     m0 + piece * 8 + lrow, rch, sg, ky, kx, cb);                             \
@@ -817,7 +823,7 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_glds_kernel(Params p)
         ph_dma(d.w, lds + (BUF_) * CF::STAGE_H + piece * 8 * BK, cx[j], (KT_) * BK * 2);     \
       }                                                                                      \
     }                                                                                        \
-    ph_kadv(p, sg, ky, kx, cb);                                                              \
+    if (live_) ph_kadv(p, sg, ky, kx, cb);                                                   \
   } while (0)
 
   f16v acc[CF::FM][CF::FN];
@@ -830,15 +836,14 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_glds_kernel(Params p)
   const int arow0 = wm * CF::TM + fr;
   const int brow0 = CF::TBM + wn * CF::TN + fr;
 
-  SDK_STAGE(kt0, 0);
-  int buf = 0;
+  // ring of NS stages: K-step kt lives in stage (kt - kt0) % NS; iteration kt refills the stage
+  // iteration kt - 1 read (its closing barrier makes that safe) with K-step kt + NS - 1
+#pragma unroll
+  for (int s = 0; s < CF::NS - 1; ++s) SDK_STAGE(kt0 + s, s);
+  int buf = 0, wbuf = CF::NS - 1;
   for (int kt = kt0; kt < kt1; ++kt) {
-    if (kt + 1 < kt1) {
-      SDK_STAGE(kt + 1, buf ^ 1);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPW) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    SDK_STAGE(kt + CF::NS - 1, wbuf);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((CF::NS - 1) * GPW) : "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
@@ -861,11 +866,13 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_glds_kernel(Params p)
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();      // everyone done reading `buf` before it is restaged
     __builtin_amdgcn_sched_barrier(0);
-    buf ^= 1;
+    buf = buf + 1 == CF::NS ? 0 : buf + 1;
+    wbuf = wbuf + 1 == CF::NS ? 0 : wbuf + 1;
   }
 #undef SDK_STAGE
-  // LDS is free: the last iteration's wait retired every DMA and its closing barrier
-  // every fragment read
+  // the trailing zero-page DMAs land before the ring is reused as epilogue scratch
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
   if (p.split == 1 && (p.out_mode == SDK_OUT_NHWC_F16 || p.out_mode == SDK_OUT_GEGLU_F16))
     epilogue_lds<CF::FM, CF::FN>(p, acc, m0, n0, wm * CF::TM, wn * CF::TN,
                                  lds + wave * (CF::LDS_BYTES / CF::NW / 16 * 8));
@@ -880,6 +887,146 @@ using Cfg128x128 = Cfg<128, 128, 2, 2>;
 using Cfg256x320 = Cfg<256, 320, 8, 2>;   // 16 waves
 using Cfg256x160 = Cfg<256, 160, 8, 1>;
 using Cfg128x320 = Cfg<128, 320, 4, 2>;
+// deeper rings for tiles whose K-step is shorter than the DMA latency (~1 us issue -> landed):
+// 128x128 (512 MFMA cycles per K-step per CU) and 256x128 / 128x256 (1024)
+using Cfg128x128r4 = Cfg<128, 128, 2, 2, 4>;   // 128 KiB
+using Cfg128x128r3 = Cfg<128, 128, 2, 2, 3>;   // 96 KiB
+using Cfg256x128r3 = Cfg<256, 128, 4, 2, 3>;   // 144 KiB
+using Cfg128x256r3 = Cfg<128, 256, 2, 4, 3>;   // 144 KiB
+
+
+// ---------------------------------------------------------------------- 16x16x32 epilogues
+// Transposed 16x16 accumulator (D^T = W A^T, v_mfma_f32_16x16x32_f16): lane l holds pixel
+// m = m_w + 16*i + (l & 15) and the 4 consecutive channels n = n_w + 32*b + 16*j + 4*(l >> 4) + q.
+// acc[i][b][j]: i = 16-pixel block (4 per 64-pixel wave half), b = 32-channel half of the wave's
+// 64 channels (GEGLU: b = 0 x, b = 1 gate), j = 16-channel block.
+constexpr int EPI16_RS = 72;                          // scratch row stride (halfs) = 144 B
+constexpr int EPI16_BYTES = 16 * EPI16_RS * 2;        // per-wave scratch: 16 pixels x 64 channels
+
+__device__ __forceinline__ void epilogue16_lds(const Params& p, f4 (&acc)[4][2][2], int m0, int n0, int m_w, int n_w,
+                                               half_t* wbuf) {
+  const int lane = threadIdx.x & 63, px = lane & 15, cg = lane >> 4;
+  const bool rb_vec = p.row_bias && !((uintptr_t)p.row_bias & 15) && !(p.rb_ld & 3);
+  half_t* out = reinterpret_cast<half_t*>(p.out);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int mt = m0 + m_w + 16 * i;                 // first pixel of the block (wave-uniform)
+    if (mt >= p.M) continue;
+    const int bw = min(mt + px, p.M - 1) / p.hw_out;  // the writer lane's image
+    if (p.out_mode == SDK_OUT_GEGLU_F16) {
+      const int nob = (n0 + n_w) / 2;                 // first output channel of the wave
+      if (nob >= p.N / 2) continue;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int nx = n0 + n_w + 16 * j + 4 * cg;    // x rows; gate rows = nx + 32
+        f4 bx = {0.f, 0.f, 0.f, 0.f}, bg = {0.f, 0.f, 0.f, 0.f};
+        if (p.bias) {
+          bx = *reinterpret_cast<const f4*>(p.bias + nx);
+          bg = *reinterpret_cast<const f4*>(p.bias + nx + 32);
+        }
+        h4 o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = (half_t)((acc[i][0][j][q] + bx[q]) * gelu_erf(acc[i][1][j][q] + bg[q]));
+        *reinterpret_cast<h4*>(wbuf + px * EPI16_RS + 16 * j + 4 * cg) = o;
+      }
+      // read back: 16 pixel rows x 32 channels = 4 lanes x 16 B per row
+      const int row = lane >> 2, c8 = lane & 3;
+      h8 v = *reinterpret_cast<const h8*>(wbuf + row * EPI16_RS + c8 * 8);
+      const int m = mt + row, no = nob + c8 * 8;
+      if (m < p.M && no < p.N / 2) {
+        if (p.res) {
+          const h8 rr = *reinterpret_cast<const h8*>(p.res + (size_t)m * p.res_ld + no);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[q] = (half_t)((float)v[q] + (float)rr[q]);
+        }
+        *reinterpret_cast<h8*>(out + (size_t)m * p.out_ld + no) = v;
+      }
+      continue;
+    }
+    if (n0 + n_w >= p.N) continue;
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = n0 + n_w + 32 * b + 16 * j + 4 * cg;
+        float v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = acc[i][b][j][q];
+        if (n < p.N) {                                // N % 8 == 0 in this mode
+          if (p.bias) {
+            const f4 bb = *reinterpret_cast<const f4*>(p.bias + n);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] += bb[q];
+          }
+          if (p.row_bias) {
+            const float* rb = p.row_bias + (size_t)bw * p.rb_ld + n;
+            if (rb_vec) {
+              const f4 r4 = *reinterpret_cast<const f4*>(rb);
+#pragma unroll
+              for (int q = 0; q < 4; ++q) v[q] += r4[q];
+            } else {
+#pragma unroll
+              for (int q = 0; q < 4; ++q) v[q] += rb[q];
+            }
+          }
+        }
+        h4 o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = (half_t)v[q];
+        *reinterpret_cast<h4*>(wbuf + px * EPI16_RS + 32 * b + 16 * j + 4 * cg) = o;
+      }
+    // read back: 16 pixel rows x 64 channels = 8 lanes x 16 B per row, 8 rows per instruction
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int row = 8 * r + (lane >> 3), c8 = lane & 7;
+      h8 v = *reinterpret_cast<const h8*>(wbuf + row * EPI16_RS + c8 * 8);
+      const int m = mt + row, n = n0 + n_w + c8 * 8;
+      if (m < p.M && n < p.N) {
+        if (p.res) {
+          const h8 rr = *reinterpret_cast<const h8*>(p.res + (size_t)m * p.res_ld + n);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[q] = (half_t)((float)v[q] + (float)rr[q]);
+        }
+        *reinterpret_cast<h8*>(out + (size_t)m * p.out_ld + n) = v;
+      }
+    }
+  }
+}
+
+// split-K fp32 slabs and the fp32 output modes (NCHW image, token rows)
+__device__ __forceinline__ void epilogue16_direct(const Params& p, f4 (&acc)[4][2][2], int m0, int n0, int m_w,
+                                                  int n_w, int split_idx) {
+  const int lane = threadIdx.x & 63, px = lane & 15, cg = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + m_w + 16 * i + px;
+    if (m >= p.M) continue;
+    const int b = m / p.hw_out;
+#pragma unroll
+    for (int b2 = 0; b2 < 2; ++b2)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = n0 + n_w + 32 * b2 + 16 * j + 4 * cg;
+        if (p.split > 1) {
+          *reinterpret_cast<f4*>(p.partial + ((size_t)split_idx * p.M + m) * p.Npad + n) = acc[i][b2][j];
+          continue;
+        }
+        float* out = reinterpret_cast<float*>(p.out);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (n + q >= p.N) continue;
+          float x = acc[i][b2][j][q];
+          if (p.bias) x += p.bias[n + q];
+          if (p.row_bias) x += p.row_bias[(size_t)b * p.rb_ld + n + q];
+          if (p.res) x += (float)p.res[(size_t)m * p.res_ld + n + q];
+          if (p.out_mode == SDK_OUT_NCHW_F32)
+            out[((size_t)b * p.N + n + q) * p.hw_out + (m - b * p.hw_out)] = x;
+          else
+            out[(size_t)m * p.out_ld + n + q] = x;
+        }
+      }
+  }
+}
 
 // ---------------------------------------------------------------------- phased LDS-DMA kernel
 // 256x256 tile, 8 waves (2 x 4), K-step 64 cut into four 16-KiB half-tiles streamed in
@@ -906,7 +1053,7 @@ struct PhCfg {
 };
 constexpr int PH_HALF = 128 * BK;   // halfs per half-tile slot
 
-template <class PC, int DBG = 0>
+template <class PC, int DBG = 0, bool M16 = false>
 __global__ void __launch_bounds__(512) conv_ph_kernel(Params p) {
   extern __shared__ __attribute__((aligned(16))) half_t lds[];
   constexpr int S = PC::S, D = PC::D;
@@ -996,27 +1143,50 @@ __global__ void __launch_bounds__(512) conv_ph_kernel(Params p) {
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
 
-  f16v acc[2][2][2];   // [A half][pixel tile][W half]
+  f16v acc[2][2][2];   // [A half][pixel tile][W half]                      (32x32x16 path)
+  f4 acc16[2][4][2][2];   // [A half][16-pixel block][W half][16-channel block] (16x16x32 path)
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int b = 0; b < 2; ++b) acc[a][i][b] = f16v{};
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc16[a][i][b][j] = f4{};
   const int fr = lane & 31, fh = lane >> 5;
-  h8 fa[2][4], fb0[4], fb1[4];
+  const int r16 = lane & 15, c16 = lane >> 4;   // 16x16x32 operand: row in block, 8-half k chunk
+  h8 fa[2][4], fb0[4], fb1[4];           // 32x32x16: [pixel tile][k16] / [k16]
+  h8 ga[4][2], gb0[2][2], gb1[2][2];     // 16x16x32: [16-pixel block][k32] / [16-channel block][k32]
 #define SDK_PH_READ_A(SLOT)                                                                \
   do {                                                                                     \
     const half_t* s_ = lds + (SLOT) * PH_HALF;                                             \
-    _Pragma("unroll") for (int i = 0; i < 2; ++i)                                          \
-      _Pragma("unroll") for (int kk = 0; kk < 4; ++kk)                                     \
-        fa[i][kk] = *reinterpret_cast<const h8*>(s_ + swz(wr * 64 + i * 32 + fr, kk * 2 + fh)); \
+    if constexpr (M16) {                                                                   \
+      _Pragma("unroll") for (int i = 0; i < 4; ++i)                                        \
+        _Pragma("unroll") for (int k = 0; k < 2; ++k)                                      \
+          ga[i][k] = *reinterpret_cast<const h8*>(s_ + swz(wr * 64 + i * 16 + r16, 4 * k + c16)); \
+    } else {                                                                               \
+      _Pragma("unroll") for (int i = 0; i < 2; ++i)                                        \
+        _Pragma("unroll") for (int kk = 0; kk < 4; ++kk)                                   \
+          fa[i][kk] = *reinterpret_cast<const h8*>(s_ + swz(wr * 64 + i * 32 + fr, kk * 2 + fh)); \
+    }                                                                                      \
   } while (0)
 #define SDK_PH_READ_B(FB, SLOT)                                                            \
   do {                                                                                     \
     const half_t* s_ = lds + (SLOT) * PH_HALF;                                             \
-    _Pragma("unroll") for (int kk = 0; kk < 4; ++kk)                                       \
-      FB[kk] = *reinterpret_cast<const h8*>(s_ + swz(wc * 32 + fr, kk * 2 + fh));           \
+    if constexpr (M16) {                                                                   \
+      _Pragma("unroll") for (int j = 0; j < 2; ++j)                                        \
+        _Pragma("unroll") for (int k = 0; k < 2; ++k)                                      \
+          g##FB[j][k] = *reinterpret_cast<const h8*>(s_ + swz(wc * 32 + j * 16 + r16, 4 * k + c16)); \
+    } else {                                                                               \
+      _Pragma("unroll") for (int kk = 0; kk < 4; ++kk)                                     \
+        f##FB[kk] = *reinterpret_cast<const h8*>(s_ + swz(wc * 32 + fr, kk * 2 + fh));     \
+    }                                                                                      \
   } while (0)
 #define SDK_PH_SYNC(NOUT)                                                                  \
   do {                                                                                     \
@@ -1028,10 +1198,18 @@ __global__ void __launch_bounds__(512) conv_ph_kernel(Params p) {
 #define SDK_PH_MMA(A, FB)                                                                  \
   do {                                                                                     \
     __builtin_amdgcn_s_setprio(1);                                                         \
-    if (!(DBG & 2)) _Pragma("unroll") for (int kk = 0; kk < 4; ++kk)                       \
-      _Pragma("unroll") for (int i = 0; i < 2; ++i)                                        \
-        acc[A][i][(FB) == 1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(                     \
-            (FB) ? fb1[kk] : fb0[kk], fa[i][kk], acc[A][i][(FB) == 1], 0, 0, 0);           \
+    if constexpr (M16) {                                                                   \
+      if (!(DBG & 2)) _Pragma("unroll") for (int k = 0; k < 2; ++k)                        \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i)                                      \
+          _Pragma("unroll") for (int j = 0; j < 2; ++j)                                    \
+            acc16[A][i][(FB) == 1][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(            \
+                (FB) ? gb1[j][k] : gb0[j][k], ga[i][k], acc16[A][i][(FB) == 1][j], 0, 0, 0); \
+    } else {                                                                               \
+      if (!(DBG & 2)) _Pragma("unroll") for (int kk = 0; kk < 4; ++kk)                     \
+        _Pragma("unroll") for (int i = 0; i < 2; ++i)                                      \
+          acc[A][i][(FB) == 1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(                   \
+              (FB) ? fb1[kk] : fb0[kk], fa[i][kk], acc[A][i][(FB) == 1], 0, 0, 0);         \
+    }                                                                                      \
     __builtin_amdgcn_s_setprio(0);                                                         \
   } while (0)
 
@@ -1048,13 +1226,13 @@ __global__ void __launch_bounds__(512) conv_ph_kernel(Params p) {
     const int g = 4 * t;
     // phase 0: (A0, W0)
     SDK_PH_READ_A(g % S);
-    SDK_PH_READ_B(fb0, (g + 1) % S);
+    SDK_PH_READ_B(b0, (g + 1) % S);
     SDK_PH_ISSUE((0 + D) & 3, (g + 0 + D) >> 2, (g + 0 + D) % S);
     SDK_PH_SYNC(D - 2);
     SDK_PH_MMA(0, 0);
     SDK_PH_BAR();
     // phase 1: (A0, W1)
-    SDK_PH_READ_B(fb1, (g + 2) % S);
+    SDK_PH_READ_B(b1, (g + 2) % S);
     SDK_PH_ISSUE((1 + D) & 3, (g + 1 + D) >> 2, (g + 1 + D) % S);
     SDK_PH_SYNC(D - 2);
     SDK_PH_MMA(0, 1);
@@ -1094,6 +1272,16 @@ __global__ void __launch_bounds__(512) conv_ph_kernel(Params p) {
   }
   // every wave past its last ring read before the ring is reused as epilogue scratch
   __builtin_amdgcn_s_barrier();
+  if constexpr (M16) {
+    if (p.split == 1 && (p.out_mode == SDK_OUT_NHWC_F16 || p.out_mode == SDK_OUT_GEGLU_F16)) {
+      epilogue16_lds(p, acc16[0], m0, n0, wr * 64, wc * 64, lds + wave * (EPI16_BYTES / 2));
+      epilogue16_lds(p, acc16[1], m0, n0, 128 + wr * 64, wc * 64, lds + wave * (EPI16_BYTES / 2));
+    } else {
+      epilogue16_direct(p, acc16[0], m0, n0, wr * 64, wc * 64, sidx);
+      epilogue16_direct(p, acc16[1], m0, n0, 128 + wr * 64, wc * 64, sidx);
+    }
+    return;
+  }
   if (p.split == 1 && (p.out_mode == SDK_OUT_NHWC_F16 || p.out_mode == SDK_OUT_GEGLU_F16)) {
     epilogue_lds<2, 2>(p, acc[0], m0, n0, wr * 64, wc * 64, lds + wave * (EPI_BYTES / 2));
     epilogue_lds<2, 2>(p, acc[1], m0, n0, 128 + wr * 64, wc * 64, lds + wave * (EPI_BYTES / 2));
@@ -1106,17 +1294,17 @@ __global__ void __launch_bounds__(512) conv_ph_kernel(Params p) {
 using PhCfg8 = PhCfg<8, 6>;
 using PhCfg10 = PhCfg<10, 8>;
 
-template <class PC, int DBG = 0>
+template <class PC, int DBG = 0, bool M16 = false>
 int launch_ph(const Params& p, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
-    if (hipFuncSetAttribute((const void*)conv_ph_kernel<PC, DBG>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (hipFuncSetAttribute((const void*)conv_ph_kernel<PC, DBG, M16>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             PC::LDS_BYTES) != hipSuccess)
       return fail(SDK_EHIP, "conv2d: cannot raise the dynamic LDS limit");
     attr_set = true;
   }
-  hipLaunchKernelGGL((conv_ph_kernel<PC, DBG>), dim3(p.tiles_m * p.tiles_n, p.split), dim3(512), PC::LDS_BYTES,
-                     s, p);
+  hipLaunchKernelGGL((conv_ph_kernel<PC, DBG, M16>), dim3(p.tiles_m * p.tiles_n, p.split), dim3(512),
+                     PC::LDS_BYTES, s, p);
   return check_launch("conv_ph");
 }
 
@@ -1285,13 +1473,16 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   // benchmarks, SDK_CONV_VARIANT=id
   const char* fe = getenv("SDK_CONV_VARIANT");
   const int forced = a->variant_hint > 0 ? a->variant_hint - 1 : (fe ? atoi(fe) : -1);
-  // ids: 0 register-staged; 2..7 LDS-DMA configs; 8, 9 phased 256x256; 10.. diagnostics
+  // ids: 0 register-staged; 2..7 LDS-DMA configs; 8, 9 phased 256x256; 10..15 diagnostics;
+  // 16..19 deep-ring LDS-DMA configs; 20, 21 phased 256x256 on v_mfma_f32_16x16x32_f16
   const int fbase = forced;
-  const bool fvalid = forced >= 0 && forced != 1 && forced <= 15;
+  const bool fvalid = forced >= 0 && forced != 1 && forced <= 21;
   const bool fgeglu = fbase <= 4 || fbase >= 8;
   if (fvalid && (forced == 0 || !transform) && (fgeglu || a->out_mode != SDK_OUT_GEGLU_F16)) {
-    static const int fbm[16] = {128, 0, 256, 256, 128, 256, 256, 128, 256, 256, 256, 256, 256, 256, 256, 256};
-    static const int fbn[16] = {128, 0, 256, 128, 128, 320, 160, 320, 256, 256, 256, 256, 256, 256, 256, 256};
+    static const int fbm[22] = {128, 0, 256, 256, 128, 256, 256, 128, 256, 256, 256, 256, 256, 256, 256, 256,
+                                128, 256, 128, 128, 256, 256};
+    static const int fbn[22] = {128, 0, 256, 128, 128, 320, 160, 320, 256, 256, 256, 256, 256, 256, 256, 256,
+                                128, 128, 128, 256, 256, 256};
     var = forced;
     tbm = fbm[fbase];
     tbn = fbn[fbase];
@@ -1302,7 +1493,7 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   p.tiles_n = (p.N + tbn - 1) / tbn;
   p.Npad = p.tiles_n * tbn;                       // split-K slab row stride
   const int tiles = p.tiles_m * p.tiles_n;
-  const int per_cu = ((var & 15) == 0 || (var & 15) == 4) ? 2 : 1;
+  const int per_cu = (var == 0 || var == 4) ? 2 : 1;
   int split = a->split_k;
   if (split <= 0) {
     if (best_split > 0) {
@@ -1366,6 +1557,12 @@ extern "C" int sdk_conv2d(const sdk_conv_args* a, sdk_stream_t stream) {
     case 13: rc = launch_ph<PhCfg8, 64>(p, s); break;  // diagnostics: no epilogue stores
     case 14: rc = launch_ph<PhCfg8, 16>(p, s); break;  // diagnostics: W from the zero page
     case 15: rc = launch_ph<PhCfg8, 32>(p, s); break;  // diagnostics: A from the zero page
+    case 16: rc = launch_glds<Cfg128x128r4>(p, s); break;
+    case 17: rc = launch_glds<Cfg256x128r3>(p, s); break;
+    case 18: rc = launch_glds<Cfg128x128r3>(p, s); break;
+    case 19: rc = launch_glds<Cfg128x256r3>(p, s); break;
+    case 20: rc = launch_ph<PhCfg8, 0, true>(p, s); break;    // phased 256x256, 16x16x32 MFMA
+    case 21: rc = launch_ph<PhCfg10, 0, true>(p, s); break;
     default:
       hipLaunchKernelGGL(conv_igemm_kernel, grid, dim3(NT), 0, s, p);
       rc = check_launch("conv_igemm");

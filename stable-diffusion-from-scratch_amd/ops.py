@@ -170,7 +170,7 @@ class _Autotune:
     Enabled by ``enable()`` (UNetModel/AutoEncoderKL.prepare(autotune=True)); the
     first call of each distinct problem times every candidate (HIP events, 3 reps
     after a warm-up) and caches the fastest.  Never runs under graph capture."""
-    VARIANTS = (2, 5, 7, 6, 4, 3, 8, 9)
+    VARIANTS = (2, 5, 7, 6, 4, 3, 8, 9, 16, 17, 18, 19, 20, 21)
     SPLITS = (0, 1, 2, 4, 8)
 
     def __init__(self):

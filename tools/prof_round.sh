@@ -19,7 +19,7 @@ step() {  # name seconds cmd...
   case $rc in 0) ;; *) echo "stopping after [$name]"; exit $rc;; esac
 }
 TUNE=$O/conv_tuning.json
-step bench 400 env BENCH_SHAPES_OUT=$O/shapes.txt python3 $R/bench.py --no-cpu-baseline --tuning-out $TUNE
+step bench 400 env BENCH_SHAPES_OUT=$O/shapes.txt BENCH_SEQ_OUT=$O/seq.json python3 $R/bench.py --no-cpu-baseline --tuning-out $TUNE
 [ -f $TUNE ] || cp $R/configs/conv_tuning_mi355x.json $TUNE
 step trace 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- \
   python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --tuning-cache $TUNE
