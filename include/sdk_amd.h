@@ -80,7 +80,8 @@ typedef struct {
   int32_t nseg;            /* 1 or 2 (segment 1 = fused 1x1 shortcut) */
   sdk_conv_src seg[2];
   const void* weight;      /* fp16 [cout_pad][k_total]; cout_pad = roundup(cout, 128);
-                              per segment: taps x roundup(cin, 64) columns, tap-major */
+                              per segment: roundup(cin, 64) / 64 channel blocks x taps x 64
+                              columns (channel-block major, tap minor) */
   int32_t k_total;
   const float* bias;       /* [cout] or NULL */
   const float* row_bias;   /* [batch][row_bias_ld] or NULL (timestep-embedding broadcast) */

@@ -77,9 +77,9 @@ __device__ __forceinline__ void load_a(const Params& p, const RowCtx& rc, int kt
                                        bool (&ok)[4], int& cglob, int& segi) {
   segi = (p.nseg > 1 && kt >= p.seg[1].kt_begin) ? 1 : 0;
   const Seg& s = p.seg[segi];
-  const int local = kt - s.kt_begin;
-  const int tap = local / s.tiles_per_tap;
-  const int c = (local - tap * s.tiles_per_tap) * BK + chunk * 8;
+  const int local = kt - s.kt_begin, taps = s.ksize * s.ksize;
+  const int cblk = local / taps, tap = local - cblk * taps;   // K order: channel block, then tap
+  const int c = cblk * BK + chunk * 8;
   const int ky = tap / s.ksize, kx = tap - ky * s.ksize;
   cglob = c;
   const bool cok = c < s.cin;
@@ -616,6 +616,146 @@ __device__ __forceinline__ void epilogue_lds(const Params& p, f16v (&acc)[FM][FN
   }
 }
 
+// ---------------------------------------------------------------------- 16x16x32 wave-tile epilogues
+// Transposed 16x16 accumulator of a TM x TN wave tile (D^T = W A^T, v_mfma_f32_16x16x32_f16):
+// acc[i][j] lane l holds pixel m_w + 16*i + (l & 15) and channels n_w + 16*j + 4*(l >> 4) + q.
+// fp16 NHWC / GEGLU: per 16-pixel block and 64-channel group (NB = 4 blocks of 16; a trailing
+// 32-channel group has NB = 2) the wave writes its fp32->fp16 values (bias, embedding, GEGLU
+// applied) to a private 16 x 72-half LDS scratch and stores 16-B row chunks (+ residual).
+constexpr int EPG_RS = 72;                          // scratch row stride (halfs) = 144 B
+constexpr int EPG_BYTES = 16 * EPG_RS * 2;          // per-wave scratch
+
+template <int NB>
+__device__ __forceinline__ void epi16_group(const Params& p, const f4* a, int mt, int nb, int bw, bool rb_vec,
+                                            half_t* wbuf) {
+  const int lane = threadIdx.x & 63, px = lane & 15, cg = lane >> 4;
+  half_t* out = reinterpret_cast<half_t*>(p.out);
+  if (p.out_mode == SDK_OUT_GEGLU_F16) {            // NB == 4: blocks 0,1 = x rows, 2,3 = gate rows
+    const int nob = nb / 2;
+    if (nob >= p.N / 2) return;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int nx = nb + 16 * j + 4 * cg;
+      f4 bx = {0.f, 0.f, 0.f, 0.f}, bg = {0.f, 0.f, 0.f, 0.f};
+      if (p.bias) {
+        bx = *reinterpret_cast<const f4*>(p.bias + nx);
+        bg = *reinterpret_cast<const f4*>(p.bias + nx + 32);
+      }
+      h4 o;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = (half_t)((a[j][q] + bx[q]) * gelu_erf(a[2 + j][q] + bg[q]));
+      *reinterpret_cast<h4*>(wbuf + px * EPG_RS + 16 * j + 4 * cg) = o;
+    }
+    const int row = lane >> 2, c8 = lane & 3;       // 16 rows x 32 channels
+    h8 v = *reinterpret_cast<const h8*>(wbuf + row * EPG_RS + c8 * 8);
+    const int m = mt + row, no = nob + c8 * 8;
+    if (m < p.M && no < p.N / 2) {
+      if (p.res) {
+        const h8 rr = *reinterpret_cast<const h8*>(p.res + (size_t)m * p.res_ld + no);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = (half_t)((float)v[q] + (float)rr[q]);
+      }
+      *reinterpret_cast<h8*>(out + (size_t)m * p.out_ld + no) = v;
+    }
+    return;
+  }
+  if (nb >= p.N) return;
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int n = nb + 16 * j + 4 * cg;
+    float v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = a[j][q];
+    if (n < p.N) {                                  // N % 8 == 0 in this mode
+      if (p.bias) {
+        const f4 bb = *reinterpret_cast<const f4*>(p.bias + n);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] += bb[q];
+      }
+      if (p.row_bias) {
+        const float* rb = p.row_bias + (size_t)bw * p.rb_ld + n;
+        if (rb_vec) {
+          const f4 r4 = *reinterpret_cast<const f4*>(rb);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] += r4[q];
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] += rb[q];
+        }
+      }
+    }
+    h4 o;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = (half_t)v[q];
+    *reinterpret_cast<h4*>(wbuf + px * EPG_RS + 16 * j + 4 * cg) = o;
+  }
+  constexpr int LPR = NB * 2, RPI = 64 / LPR;       // lanes per row, rows per instruction
+#pragma unroll
+  for (int r = 0; r < 16 / RPI; ++r) {
+    const int row = r * RPI + lane / LPR, c8 = lane % LPR;
+    h8 v = *reinterpret_cast<const h8*>(wbuf + row * EPG_RS + c8 * 8);
+    const int m = mt + row, n = nb + c8 * 8;
+    if (m < p.M && n < p.N) {
+      if (p.res) {
+        const h8 rr = *reinterpret_cast<const h8*>(p.res + (size_t)m * p.res_ld + n);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = (half_t)((float)v[q] + (float)rr[q]);
+      }
+      *reinterpret_cast<h8*>(out + (size_t)m * p.out_ld + n) = v;
+    }
+  }
+}
+
+template <int FM, int FN>
+__device__ __forceinline__ void epilogue16_tile(const Params& p, f4 (&acc)[FM][FN], int m0, int n0, int m_w, int n_w,
+                                                half_t* wbuf) {
+  const int lane = threadIdx.x & 63, px = lane & 15;
+  const bool rb_vec = p.row_bias && !((uintptr_t)p.row_bias & 15) && !(p.rb_ld & 3);
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int mt = m0 + m_w + 16 * i;
+    if (mt >= p.M) continue;
+    const int bw = min(mt + px, p.M - 1) / p.hw_out;
+#pragma unroll
+    for (int g = 0; g < FN / 4; ++g) epi16_group<4>(p, &acc[i][4 * g], mt, n0 + n_w + 64 * g, bw, rb_vec, wbuf);
+    if constexpr (FN % 4 == 2) epi16_group<2>(p, &acc[i][FN - 2], mt, n0 + n_w + 16 * (FN - 2), bw, rb_vec, wbuf);
+  }
+}
+
+// split-K fp32 slabs and the fp32 output modes (NCHW image, token rows)
+template <int FM, int FN>
+__device__ __forceinline__ void epilogue16_tile_direct(const Params& p, f4 (&acc)[FM][FN], int m0, int n0, int m_w,
+                                                       int n_w, int split_idx) {
+  const int lane = threadIdx.x & 63, px = lane & 15, cg = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int m = m0 + m_w + 16 * i + px;
+    if (m >= p.M) continue;
+    const int b = m / p.hw_out;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + n_w + 16 * j + 4 * cg;
+      if (p.split > 1) {
+        *reinterpret_cast<f4*>(p.partial + ((size_t)split_idx * p.M + m) * p.Npad + n) = acc[i][j];
+        continue;
+      }
+      float* out = reinterpret_cast<float*>(p.out);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (n + q >= p.N) continue;
+        float x = acc[i][j][q];
+        if (p.bias) x += p.bias[n + q];
+        if (p.row_bias) x += p.row_bias[(size_t)b * p.rb_ld + n + q];
+        if (p.res) x += (float)p.res[(size_t)m * p.res_ld + n + q];
+        if (p.out_mode == SDK_OUT_NCHW_F32)
+          out[((size_t)b * p.N + n + q) * p.hw_out + (m - b * p.hw_out)] = x;
+        else
+          out[(size_t)m * p.out_ld + n + q] = x;
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------- LDS-DMA kernel
 // A and W tiles are loaded straight into LDS with global_load_lds_dwordx4 (one
 // 1-KiB wave instruction = 8 rows x 128 B); the per-lane SOURCE address carries
@@ -628,13 +768,15 @@ __device__ __forceinline__ void epilogue_lds(const Params& p, f16v (&acc)[FM][FN
 // applied by gn_apply before 3x3 convs); every segment must be transform-free.
 __device__ __attribute__((aligned(16))) half_t g_zero_page[8];
 
-template <int BM_, int BN_, int WM_, int WN_, int NS_ = 2>
+template <int BM_, int BN_, int WM_, int WN_, int NS_ = 2, bool M16_ = false>
 struct Cfg {
   static constexpr int TBM = BM_, TBN = BN_, WM = WM_, WN = WN_;
   static constexpr int NS = NS_;                         // LDS ring stages (NS - 1 K-steps of DMA in flight)
+  static constexpr bool M16 = M16_;                      // v_mfma_f32_16x16x32_f16 instead of 32x32x16
   static constexpr int NW = WM * WN, NT = NW * 64;
   static constexpr int TM = TBM / WM, TN = TBN / WN;
   static constexpr int FM = TM / 32, FN = TN / 32;
+  static constexpr int FM16 = TM / 16, FN16 = TN / 16;
   static constexpr int ROWS = TBM + TBN;                 // LDS rows (128 B) per stage
   static constexpr int STAGE_H = ROWS * BK;              // halfs per stage
   static constexpr int NINSTR = ROWS / 8;                // 1-KiB DMA pieces per stage
@@ -662,26 +804,30 @@ __device__ __forceinline__ void ph_dma(__amdgpu_buffer_rsrc_t r, half_t* dst, un
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)dst, 16, voff, soff, 0, 0);
 }
 
-// K-step -> (segment, tap row, tap column, channel base); scalar.
+// K-step -> (segment, tap row, tap column, channel base); scalar.  K order inside a
+// segment: 64-channel block major, tap minor — the nine taps of one channel block read
+// overlapping pixel windows back to back, so a 3x3 conv re-reads its A tile from L2
+// (a workgroup's window over one block is ~48 KiB) instead of after a sweep over all
+// channels (which overflows the 4 MiB L2 of an XCD at the 64x64 level).
 __device__ __forceinline__ void ph_kstate(const Params& p, int kt, int& seg, int& ky, int& kx, int& cb) {
   const bool s1 = p.nseg > 1 && kt >= p.seg[1].kt_begin;
   seg = s1 ? 1 : 0;
-  const int local = kt - SDK_SEGF(kt_begin), tpt = SDK_SEGF(tiles_per_tap), ks = SDK_SEGF(ksize);
-  const int tap = local / tpt;
-  cb = (local - tap * tpt) * BK;
+  const int local = kt - SDK_SEGF(kt_begin), ks = SDK_SEGF(ksize), taps = ks * ks;
+  const int cblk = local / taps, tap = local - cblk * taps;
+  cb = cblk * BK;
   ky = tap / ks;
   kx = tap - ky * ks;
 }
 
 __device__ __forceinline__ void ph_kadv(const Params& p, int& seg, int& ky, int& kx, int& cb) {
   const bool s1 = seg != 0;
-  cb += BK;
-  if (cb >= SDK_SEGF(cin_pad)) {
-    cb = 0;
-    const int ks = SDK_SEGF(ksize);
-    if (++kx == ks) {
-      kx = 0;
-      if (++ky == ks) { ky = 0; ++seg; }
+  const int ks = SDK_SEGF(ksize);
+  if (++kx == ks) {
+    kx = 0;
+    if (++ky == ks) {
+      ky = 0;
+      cb += BK;
+      if (cb >= SDK_SEGF(cin_pad)) { cb = 0; ++seg; }
     }
   }
 }
@@ -827,14 +973,25 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_glds_kernel(Params p)
   } while (0)
 
   f16v acc[CF::FM][CF::FN];
+  f4 acc16[CF::FM16][CF::FN16];
+  if constexpr (CF::M16) {
 #pragma unroll
-  for (int i = 0; i < CF::FM; ++i)
+    for (int i = 0; i < CF::FM16; ++i)
 #pragma unroll
-    for (int j = 0; j < CF::FN; ++j) acc[i][j] = f16v{};
+      for (int j = 0; j < CF::FN16; ++j) acc16[i][j] = f4{};
+  } else {
+#pragma unroll
+    for (int i = 0; i < CF::FM; ++i)
+#pragma unroll
+      for (int j = 0; j < CF::FN; ++j) acc[i][j] = f16v{};
+  }
 
   const int fr = lane & 31, fh = lane >> 5;
   const int arow0 = wm * CF::TM + fr;
   const int brow0 = CF::TBM + wn * CF::TN + fr;
+  const int r16 = lane & 15, c16 = lane >> 4;   // 16x16x32 operand: row in block, 8-half K chunk
+  const int arow16 = wm * CF::TM + r16;
+  const int brow16 = CF::TBM + wn * CF::TN + r16;
 
   // ring of NS stages: K-step kt lives in stage (kt - kt0) % NS; iteration kt refills the stage
   // iteration kt - 1 read (its closing barrier makes that safe) with K-step kt + NS - 1
@@ -848,6 +1005,24 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_glds_kernel(Params p)
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     const half_t* st = lds + buf * CF::STAGE_H;
+    if constexpr (CF::M16) {
+#pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk) {
+        h8 fa[CF::FM16];
+#pragma unroll
+        for (int i = 0; i < CF::FM16; ++i)
+          fa[i] = *reinterpret_cast<const h8*>(st + swz(arow16 + i * 16, kk * 4 + c16));
+        // one W fragment at a time: the 32x160 wave tiles of the 16-wave configs keep
+        // 80 accumulator VGPRs and must stay within 128
+#pragma unroll
+        for (int j = 0; j < CF::FN16; ++j) {
+          const h8 fb = *reinterpret_cast<const h8*>(st + swz(brow16 + j * 16, kk * 4 + c16));
+#pragma unroll
+          for (int i = 0; i < CF::FM16; ++i)
+            acc16[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb, fa[i], acc16[i][j], 0, 0, 0);
+        }
+      }
+    } else
 #pragma unroll
     for (int kk = 0; kk < BK / 16; ++kk) {
       h8 fa[CF::FM], fb[CF::FN];
@@ -873,6 +1048,14 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_glds_kernel(Params p)
   // the trailing zero-page DMAs land before the ring is reused as epilogue scratch
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
+  if constexpr (CF::M16) {
+    if (p.split == 1 && (p.out_mode == SDK_OUT_NHWC_F16 || p.out_mode == SDK_OUT_GEGLU_F16))
+      epilogue16_tile<CF::FM16, CF::FN16>(p, acc16, m0, n0, wm * CF::TM, wn * CF::TN,
+                                          lds + wave * (CF::LDS_BYTES / CF::NW / 16 * 8));
+    else
+      epilogue16_tile_direct<CF::FM16, CF::FN16>(p, acc16, m0, n0, wm * CF::TM, wn * CF::TN, sidx);
+    return;
+  }
   if (p.split == 1 && (p.out_mode == SDK_OUT_NHWC_F16 || p.out_mode == SDK_OUT_GEGLU_F16))
     epilogue_lds<CF::FM, CF::FN>(p, acc, m0, n0, wm * CF::TM, wn * CF::TN,
                                  lds + wave * (CF::LDS_BYTES / CF::NW / 16 * 8));
@@ -893,6 +1076,13 @@ using Cfg128x128r4 = Cfg<128, 128, 2, 2, 4>;   // 128 KiB
 using Cfg128x128r3 = Cfg<128, 128, 2, 2, 3>;   // 96 KiB
 using Cfg256x128r3 = Cfg<256, 128, 4, 2, 3>;   // 144 KiB
 using Cfg128x256r3 = Cfg<128, 256, 2, 4, 3>;   // 144 KiB
+// the same tiles on v_mfma_f32_16x16x32_f16 (on random data the 16x16 shape holds a higher clock
+// under load than 32x32 at equal cycles per FLOP: MI355X_MICROARCH.md 'DVFS give-back' (7))
+using Cfg256x320m = Cfg<256, 320, 8, 2, 2, true>;
+using Cfg128x320m = Cfg<128, 320, 4, 2, 2, true>;
+using Cfg256x160m = Cfg<256, 160, 8, 1, 2, true>;
+using Cfg128x256r3m = Cfg<128, 256, 2, 4, 3, true>;
+using Cfg128x128r3m = Cfg<128, 128, 2, 2, 3, true>;
 
 
 // ---------------------------------------------------------------------- 16x16x32 epilogues
@@ -1474,15 +1664,16 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   const char* fe = getenv("SDK_CONV_VARIANT");
   const int forced = a->variant_hint > 0 ? a->variant_hint - 1 : (fe ? atoi(fe) : -1);
   // ids: 0 register-staged; 2..7 LDS-DMA configs; 8, 9 phased 256x256; 10..15 diagnostics;
-  // 16..19 deep-ring LDS-DMA configs; 20, 21 phased 256x256 on v_mfma_f32_16x16x32_f16
+  // 16..19 deep-ring LDS-DMA configs; 20, 21 phased 256x256 on v_mfma_f32_16x16x32_f16;
+  // 22..26 LDS-DMA configs 5, 7, 6, 19, 18 on v_mfma_f32_16x16x32_f16
   const int fbase = forced;
-  const bool fvalid = forced >= 0 && forced != 1 && forced <= 21;
-  const bool fgeglu = fbase <= 4 || fbase >= 8;
+  const bool fvalid = forced >= 0 && forced != 1 && forced <= 26;
+  const bool fgeglu = (fbase <= 4 || fbase >= 8) && fbase != 22 && fbase != 23 && fbase != 24;
   if (fvalid && (forced == 0 || !transform) && (fgeglu || a->out_mode != SDK_OUT_GEGLU_F16)) {
-    static const int fbm[22] = {128, 0, 256, 256, 128, 256, 256, 128, 256, 256, 256, 256, 256, 256, 256, 256,
-                                128, 256, 128, 128, 256, 256};
-    static const int fbn[22] = {128, 0, 256, 128, 128, 320, 160, 320, 256, 256, 256, 256, 256, 256, 256, 256,
-                                128, 128, 128, 256, 256, 256};
+    static const int fbm[27] = {128, 0, 256, 256, 128, 256, 256, 128, 256, 256, 256, 256, 256, 256, 256, 256,
+                                128, 256, 128, 128, 256, 256, 256, 128, 256, 128, 128};
+    static const int fbn[27] = {128, 0, 256, 128, 128, 320, 160, 320, 256, 256, 256, 256, 256, 256, 256, 256,
+                                128, 128, 128, 256, 256, 256, 320, 320, 160, 256, 128};
     var = forced;
     tbm = fbm[fbase];
     tbn = fbn[fbase];
@@ -1563,6 +1754,11 @@ extern "C" int sdk_conv2d(const sdk_conv_args* a, sdk_stream_t stream) {
     case 19: rc = launch_glds<Cfg128x256r3>(p, s); break;
     case 20: rc = launch_ph<PhCfg8, 0, true>(p, s); break;    // phased 256x256, 16x16x32 MFMA
     case 21: rc = launch_ph<PhCfg10, 0, true>(p, s); break;
+    case 22: rc = launch_glds<Cfg256x320m>(p, s); break;
+    case 23: rc = launch_glds<Cfg128x320m>(p, s); break;
+    case 24: rc = launch_glds<Cfg256x160m>(p, s); break;
+    case 25: rc = launch_glds<Cfg128x256r3m>(p, s); break;
+    case 26: rc = launch_glds<Cfg128x128r3m>(p, s); break;
     default:
       hipLaunchKernelGGL(conv_igemm_kernel, grid, dim3(NT), 0, s, p);
       rc = check_launch("conv_igemm");

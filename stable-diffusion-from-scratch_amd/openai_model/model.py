@@ -254,13 +254,12 @@ class UNetModel(nn.Module):
         self.out = nn.Sequential(normalization(ch), nn.SiLU(),
                                  zero_module(conv_nd(dims, model_channels, out_channels, 3, padding=1)))
         self._prepared_on = None
-        self._ctx_key = None
-        self._ctx_kv = None
+        self._ctx_cache = None
 
     # ------------------------------------------------------------------ packing
     def load_state_dict(self, *args, **kwargs):
         self._prepared_on = None
-        self._ctx_key = None
+        self._ctx_cache = None
         return super().load_state_dict(*args, **kwargs)
 
     @torch.no_grad()
@@ -294,14 +293,14 @@ class UNetModel(nn.Module):
         self._freqs = timestep_frequencies(self.model_channels).to(dev)
         self._sts = [m for m in self.modules() if isinstance(m, SpatialTransformer)]
         self._prepared_on = dev
-        self._ctx_key = None
+        self._ctx_cache = None
 
     def _context_kv(self, context):
         if context is None:
             return None, None
         key = (context.data_ptr(), context._version, tuple(context.shape), context.dtype)
-        if self._ctx_key == key:
-            return self._ctx_kv, context.shape[1]
+        if self._ctx_cache is not None and key in self._ctx_cache:
+            return self._ctx_cache[key], context.shape[1]
         B, L, D = context.shape
         if context.dtype == torch.float16:
             c2 = context.reshape(B * L, D).contiguous()
@@ -310,7 +309,10 @@ class UNetModel(nn.Module):
         kv = {}
         for st in self._sts:
             kv[id(st)] = st.context_kv(c2)
-        self._ctx_key, self._ctx_kv = key, kv
+        # a few contexts stay cached (the batch halves of a two-lane step, cond / uncond)
+        if self._ctx_cache is None or len(self._ctx_cache) >= 4:
+            self._ctx_cache = {}
+        self._ctx_cache[key] = kv
         return kv, L
 
     # ------------------------------------------------------------------ forward

@@ -40,14 +40,29 @@ def _need_cuda(t: torch.Tensor, what: str, dtype=torch.float16):
 # --------------------------------------------------------------------------- workspace
 
 class _Workspace:
-    """One growable per-device scratch buffer (split-K slabs, GroupNorm partials).
-    Calls are stream-ordered on one stream, so a single buffer is safe to reuse."""
+    """Growable scratch buffers (split-K slabs, GroupNorm partials), one per (device, lane).
+    Calls of one lane are stream-ordered on one stream, so its buffer is safe to reuse;
+    work issued concurrently on another stream must run under another lane
+    (``with WORKSPACE.use_lane(i)``)."""
 
     def __init__(self):
         self.buf = {}
+        self.lane = 0
+
+    def use_lane(self, lane: int):
+        import contextlib
+
+        @contextlib.contextmanager
+        def cm():
+            prev, self.lane = self.lane, lane
+            try:
+                yield
+            finally:
+                self.lane = prev
+        return cm()
 
     def get(self, nbytes: int, device) -> torch.Tensor:
-        key = torch.device(device).index
+        key = (torch.device(device).index, self.lane)
         b = self.buf.get(key)
         if b is None or b.numel() < nbytes:
             if torch.cuda.is_current_stream_capturing():
@@ -112,7 +127,7 @@ class PackedConv:
     ``segments``: list of (weight [N, Cin, k, k] or [N, Cin], cin_src) — cin_src is
     the channel count of the NHWC source feeding that segment (>= Cin; extra
     channels get zero weights).  Packed layout: fp16 [roundup(N,128)][sum_s k*k*roundup(cin_src,64)],
-    tap-major then channel.  ``geglu`` interleaves the (x, gate) halves of a
+    per segment 64-channel block major, then tap, then channel.  ``geglu`` interleaves the (x, gate) halves of a
     GEGLU projection in 32-row groups so one wave holds both.
     """
 
@@ -133,6 +148,8 @@ class PackedConv:
             cin_pad = (cin_src + BK - 1) // BK * BK
             wp = torch.zeros(N, kh, kw, cin_pad, dtype=torch.float32, device=w.device)
             wp[:, :, :, :Cin] = w.permute(0, 2, 3, 1)
+            # K order: 64-channel block major, tap minor (the kernels' K-step order)
+            wp = wp.reshape(N, kh * kw, cin_pad // BK, BK).permute(0, 2, 1, 3)
             cols.append(wp.reshape(N, -1))
             self.seg_geom.append((kh, cin_src))
         Wt = torch.cat(cols, dim=1)
@@ -170,7 +187,7 @@ class _Autotune:
     Enabled by ``enable()`` (UNetModel/AutoEncoderKL.prepare(autotune=True)); the
     first call of each distinct problem times every candidate (HIP events, 3 reps
     after a warm-up) and caches the fastest.  Never runs under graph capture."""
-    VARIANTS = (2, 5, 7, 6, 4, 3, 8, 9, 16, 17, 18, 19, 20, 21)
+    VARIANTS = (2, 5, 7, 6, 4, 3, 8, 9, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26)
     SPLITS = (0, 1, 2, 4, 8)
 
     def __init__(self):

@@ -42,7 +42,8 @@ def _conv_ref(x_nhwc, w, b, stride=1, pad=1, upsample=False, gn=None, silu=False
     return F.conv2d(x, w.float(), None if b is None else b.float(), stride=stride, padding=pad).permute(0, 2, 3, 1)
 
 
-@pytest.fixture(params=["auto", "0", "2", "3", "4", "5", "6", "7", "8", "9", "16", "17", "18", "19"])
+@pytest.fixture(params=["auto", "0", "2", "3", "4", "5", "6", "7", "8", "9", "16", "17", "18", "19", "20", "21",
+                        "22", "23", "24", "25", "26"])
 def conv_variant(request):
     """Every conv kernel variant (register-staged 128x128, LDS-DMA 256x256/256x128/128x128)."""
     import os
