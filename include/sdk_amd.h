@@ -66,6 +66,8 @@ typedef struct {
   const float* gn_scale;   /* [batch][cin] or NULL */
   const float* gn_shift;   /* [batch][cin] or NULL */
   int32_t silu;            /* apply x*sigmoid(x) after the affine */
+  int32_t pad_end;         /* extra zero rows/cols after the source (bottom/right) on top of pad:
+                              the KL-VAE Downsample's F.pad(x, (0,1,0,1)) + conv s2 p0 (Unet/unet.py:64-68) */
 } sdk_conv_src;
 
 enum sdk_out_mode {
@@ -191,6 +193,20 @@ int sdk_timestep_embedding(const int64_t* t, const float* freqs, void* out, int3
  * (x.type(dtype), model.py:572; 1/scale_factor*z, ldm/diffusion/ddpm.py:1095). */
 int sdk_nchw_to_nhwc(const float* x, void* y, int32_t batch, int32_t channels, int32_t hw, int32_t c_pad,
                      float scale, sdk_stream_t stream);
+
+/* KL posterior sample scaled into the diffusion latent space:
+ * z = scale * (mean + exp(0.5 * clamp(logvar, -30, 20)) * noise), or scale * mean when noise is NULL
+ * (the posterior mode).  moments: NCHW fp32 [batch][2*channels][hw] (mean | logvar, the quant_conv
+ * output), z: [batch][channels][hw].  Replaces DiagonalGaussianDistribution.sample/mode
+ * (Distribution/distribution.py:31-50) + get_first_stage_encoding's scale (ldm/diffusion/ddpm.py:795-806). */
+int sdk_diag_gaussian_sample(const float* moments, const float* noise, float* z, int32_t batch, int32_t channels,
+                             int32_t hw, float scale, sdk_stream_t stream);
+
+/* DDIM stochastic encode (ldm/diffusion/ddim.py:209-222 == DDIM/ddim.py:207-220) for one timestep:
+ * out = sqrt_a * x0 + sqrt_1ma * noise, two correctly-rounded products and a sum (no contraction),
+ * bit-identical to torch's CPU evaluation of the reference expression. */
+int sdk_stochastic_encode(const float* x0, const float* noise, float* out, int64_t n, float sqrt_a,
+                          float sqrt_1ma, sdk_stream_t stream);
 
 /* ---------------------------------------------------------------- introspection */
 const char* sdk_last_error(void);

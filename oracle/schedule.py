@@ -194,3 +194,24 @@ def ddpm_step(image: np.ndarray, eps: np.ndarray, sc: dict, noise: np.ndarray | 
     if noise is not None and sc["sigma"] != 0:
         out = out + sc["sigma"] * noise.astype(F32)
     return out.astype(F32)
+
+
+def stochastic_encode(x0: np.ndarray, noise: np.ndarray, tab: dict, index: int) -> np.ndarray:
+    """DDIMSampler.stochastic_encode at DDIM index t (``ldm/diffusion/ddim.py:209-222``):
+    sqrt(ddim_alphas)[t] * x0 + ddim_sqrt_one_minus_alphas[t] * noise, fp32, op by op."""
+    f32 = np.float32
+    sa = np.sqrt(f32(tab["ddim_alphas"][index]), dtype=f32)
+    s1m = f32(tab["ddim_sqrt_one_minus_alphas"][index])
+    return (sa * x0.astype(f32)).astype(f32) + (s1m * noise.astype(f32)).astype(f32)
+
+
+def ddim_decode(x_latent: np.ndarray, eps_fn, tab: dict, t_start: int) -> np.ndarray:
+    """DDIMSampler.decode (``ldm/diffusion/ddim.py:224-241``): the first ``t_start`` DDIM
+    timesteps walked in reverse, index = t_start - i - 1, one p_sample_ddim update each."""
+    ts = tab["ddim_timesteps"][:t_start]
+    x = x_latent.astype(F32)
+    for i, step in enumerate(np.flip(ts)):
+        index = t_start - i - 1
+        e = eps_fn(x, np.full((x.shape[0],), int(step), dtype=np.int64))
+        x, _ = ddim_step(x, e, ddim_step_scalars(tab, index))
+    return x

@@ -12,6 +12,13 @@ Follows (file:line into /root/reference):
   8 heads × C/8, default scale d^-½, proj_out, + x) — ``Unet/attention.py:221-264``.
 * ``decode_first_stage`` scaling z / scale_factor — ``ldm/diffusion/ddpm.py:1095``
   (the ``Diffusion/ddpm.py:728`` variant drops z).
+* Encode: ``Encoder.__init__/forward`` — ``Encoder_Decoder/encoder.py:20-103``
+  (conv_in → per level num_res_blocks ResnetBlocks (+attn) and Downsample except at the last
+  level → mid → norm_out → SiLU → conv_out), ``Downsample`` F.pad(0,1,0,1) + conv3×3 s2 p0 —
+  ``Unet/unet.py:52-71``; ``AutoEncoderKL.encode`` quant_conv 1×1 → posterior —
+  ``VAE/autoencoder.py:114-123``; ``DiagonalGaussianDistribution`` (logvar clamp [-30, 20],
+  std = exp(logvar/2), sample = mean + std·noise) — ``Distribution/distribution.py:31-50``;
+  ``get_first_stage_encoding`` scale_factor·z — ``ldm/diffusion/ddpm.py:795-806``.
 """
 from __future__ import annotations
 
@@ -109,3 +116,60 @@ def autoencoder_decode(sd: dict, ddconfig: dict, z: torch.Tensor) -> torch.Tenso
 @torch.no_grad()
 def decode_first_stage(sd: dict, ddconfig: dict, z: torch.Tensor, scale_factor: float) -> torch.Tensor:
     return autoencoder_decode(sd, ddconfig, 1.0 / scale_factor * z.float())
+
+
+def encoder_layout(ddconfig: dict) -> list:
+    ch, mult = ddconfig["ch"], list(ddconfig["ch_mult"])
+    in_mult = (1,) + tuple(mult)
+    curr_res = ddconfig["resolution"]
+    levels = []
+    for i_level in range(len(mult)):
+        block_in, block_out = ch * in_mult[i_level], ch * mult[i_level]
+        blocks, attn = [], []
+        for _ in range(ddconfig["num_res_blocks"]):
+            blocks.append((block_in, block_out))
+            block_in = block_out
+            if curr_res in ddconfig.get("attn_resolutions", []):
+                attn.append(block_in)
+        down = i_level != len(mult) - 1
+        if down:
+            curr_res //= 2
+        levels.append({"blocks": blocks, "attn": attn, "downsample": down})
+    return levels
+
+
+@torch.no_grad()
+def encoder_forward(sd: dict, ddconfig: dict, x: torch.Tensor, prefix="encoder") -> torch.Tensor:
+    sd = {k: v.float() for k, v in sd.items()}
+    p = prefix
+    h = _conv(x.float(), sd, p + ".conv_in")
+    for i_level, lv in enumerate(encoder_layout(ddconfig)):
+        for i_block in range(len(lv["blocks"])):
+            h = resnet_block(sd, f"{p}.down.{i_level}.block.{i_block}", h)
+            if lv["attn"]:
+                h = flash_attention_block(sd, f"{p}.down.{i_level}.attn.{i_block}", h)
+        if lv["downsample"]:
+            h = F.pad(h, (0, 1, 0, 1), mode="constant", value=0)
+            w = sd[f"{p}.down.{i_level}.downsample.conv.weight"]
+            h = F.conv2d(h, w, sd[f"{p}.down.{i_level}.downsample.conv.bias"], stride=2, padding=0)
+    h = resnet_block(sd, p + ".mid.block_1", h)
+    h = flash_attention_block(sd, p + ".mid.attn_1", h)
+    h = resnet_block(sd, p + ".mid.block_2", h)
+    return _conv(F.silu(_gn(h, sd, p + ".norm_out", 1e-6)), sd, p + ".conv_out")
+
+
+@torch.no_grad()
+def autoencoder_moments(sd: dict, ddconfig: dict, x: torch.Tensor) -> torch.Tensor:
+    """AutoEncoderKL.encode up to the posterior parameters: quant_conv(encoder(x))."""
+    sd32 = {k: v.float() for k, v in sd.items()}
+    h = encoder_forward(sd32, ddconfig, x)
+    return F.conv2d(h, sd32["quant_conv.weight"], sd32["quant_conv.bias"])
+
+
+def posterior_sample(moments: torch.Tensor, noise=None, scale_factor: float = 1.0) -> torch.Tensor:
+    """scale_factor * DiagonalGaussianDistribution(moments).sample() with the given noise (mode if None)."""
+    mean, logvar = torch.chunk(moments.float(), 2, dim=1)
+    if noise is None:
+        return scale_factor * mean
+    std = torch.exp(0.5 * torch.clamp(logvar, -30.0, 20.0))
+    return scale_factor * (mean + std * noise)

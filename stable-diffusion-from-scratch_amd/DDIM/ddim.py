@@ -138,3 +138,52 @@ class DDIMSampler(object):
         return ops.ddim_step(x.float().contiguous(), e_t, sc, noise=noise if sc["sigma"] != 0.0 else None,
                              e_uncond=e_u, guidance=unconditional_guidance_scale, v_param=v,
                              temperature=temperature)
+
+    # ------------------------------------------------------------------ img2img
+    @torch.no_grad()
+    def stochastic_encode(self, x0, t, use_original_steps=False, noise=None):
+        """q(x_t | x0) at DDIM index t (``ddim.py:207-220``): sqrt(a_t)·x0 + sqrt(1-a_t)·noise, fp32 op
+        by op on the device (``sdk_stochastic_encode``) — bit-identical to the reference expression.
+        ``t`` holds DDIM indices per sample (original 1000-step indices with ``use_original_steps``)."""
+        if use_original_steps:
+            ac = self.model.alphas_cumprod.detach().to("cpu", torch.float32).numpy()
+            sa_tab = np.sqrt(ac)
+            s1m_tab = np.sqrt((np.float32(1.0) - ac).astype(np.float32))
+        else:
+            sa_tab = np.sqrt(self.ddim_alphas.numpy().astype(np.float32))
+            s1m_tab = self.ddim_sqrt_one_minus_alphas.numpy().astype(np.float32)
+        x0 = x0.float().contiguous()
+        if noise is None:
+            noise = torch.randn_like(x0)
+        noise = noise.to(device=x0.device, dtype=torch.float32).contiguous()
+        tt = torch.as_tensor(t).reshape(-1).to("cpu", torch.long)
+        if tt.numel() == 1:
+            tt = tt.expand(x0.shape[0])
+        out = torch.empty_like(x0)
+        vals = tt.unique()
+        if vals.numel() == 1:
+            i = int(vals[0])
+            return ops.stochastic_encode(x0, noise, float(sa_tab[i]), float(s1m_tab[i]), out=out)
+        for b in range(x0.shape[0]):                 # per-sample timesteps: one launch per sample
+            i = int(tt[b])
+            ops.stochastic_encode(x0[b], noise[b], float(sa_tab[i]), float(s1m_tab[i]), out=out[b])
+        return out
+
+    @torch.no_grad()
+    def decode(self, x_latent, cond, t_start, unconditional_guidance_scale=1.0, unconditional_conditioning=None,
+               use_original_steps=False):
+        """Denoise from DDIM index ``t_start`` (``ddim.py:222-240``): timesteps[:t_start] walked in
+        reverse, index = total_steps - i - 1, one fused HIP update per step."""
+        if use_original_steps:
+            raise NotImplementedError("sd_amd: original-steps decoding is not on the img2img path")
+        timesteps = self.ddim_timesteps[:t_start]
+        time_range = np.flip(timesteps)
+        total_steps = timesteps.shape[0]
+        x_dec = x_latent.float().contiguous()
+        for i, step in enumerate(time_range):
+            index = total_steps - i - 1
+            ts = torch.full((x_latent.shape[0],), int(step), device=x_latent.device, dtype=torch.long)
+            x_dec, _ = self.p_sample_ddim(x_dec, cond, ts, index=index, use_original_steps=use_original_steps,
+                                          unconditional_guidance_scale=unconditional_guidance_scale,
+                                          unconditional_conditioning=unconditional_conditioning)
+        return x_dec

@@ -79,5 +79,19 @@ class LatentDiffusion(nn.Module):
         return self.model(x_noisy, t, **cond)
 
     @torch.no_grad()
+    def encode_first_stage(self, x):
+        """``ldm/diffusion/ddpm.py:1237-1279`` (non-split branch): the first stage's posterior."""
+        return self.first_stage_model.encode(x)
+
+    def get_first_stage_encoding(self, encoder_posterior, noise=None):
+        """``ldm/diffusion/ddpm.py:795-806``: scale_factor * posterior sample (fused on the device)."""
+        from ..Distribution.distribution import DiagonalGaussianDistribution
+        if isinstance(encoder_posterior, DiagonalGaussianDistribution):
+            return encoder_posterior.sample_scaled(self.scale_factor, noise=noise)
+        if isinstance(encoder_posterior, torch.Tensor):
+            return self.scale_factor * encoder_posterior
+        raise NotImplementedError(f"encoder_posterior of type '{type(encoder_posterior)}' not yet implemented")
+
+    @torch.no_grad()
     def decode_first_stage(self, z, predict_cids=False, force_not_quantize=False):
         return self.first_stage_model.decode(z, pre_scale=1.0 / self.scale_factor)

@@ -1,5 +1,10 @@
-"""Mirror of ``Encoder_Decoder/encoder.py`` — KL-VAE Decoder (HIP-backed) and the Encoder's
-parameter layout (so full AutoEncoderKL state_dicts load; encode is outside this round's scope).
+"""Mirror of ``Encoder_Decoder/encoder.py`` — KL-VAE Encoder and Decoder (HIP-backed).
+
+Encoder walk (``encoder.py:20-103``): conv_in → per level num_res_blocks ResnetBlocks
+(attention at ``attn_resolutions``) and a Downsample (asymmetric pad, stride 2) except at
+the last level → mid(block_1, attn_1, block_2) → norm_out → SiLU → conv_out.  conv_out is
+folded with AutoEncoderKL.quant_conv (1x1, no nonlinearity between them) into one conv that
+writes the NCHW fp32 posterior moments directly.
 
 Decoder walk (``encoder.py:106-210``): conv_in → mid(block_1, attn_1, block_2) →
 levels reversed (num_res_blocks+1 ResnetBlocks each, attention at
@@ -63,8 +68,50 @@ class Encoder(nn.Module):
         self.conv_out = nn.Conv2d(block_in, 2 * z_channels if double_z else z_channels, kernel_size=3, stride=1,
                                   padding=1)
 
+        self._block_out = block_in
+
+    def _prepare(self, dev, in_pad, quant_conv=None):
+        """Pack every conv; conv_out is folded with ``quant_conv`` (1x1) when given:
+        W = Wq·Wout, b = Wq·b_out + b_q (fp32 on the host, then fp16)."""
+        self._in_pad = in_pad
+        self._pc_in = ops.PackedConv([(self.conv_in.weight, in_pad)], self.conv_in.bias, device=dev)
+        for m in self.modules():
+            if m is not self and hasattr(m, "_prepare") and not isinstance(m, (Encoder, Decoder)):
+                m._prepare(dev)
+        _gn_prep(self.norm_out, dev)
+        w, b = self.conv_out.weight.detach().float(), self.conv_out.bias.detach().float()
+        if quant_conv is not None:
+            wq = quant_conv.weight.detach().float()[:, :, 0, 0]
+            w = torch.einsum("nj,jcyx->ncyx", wq, w)
+            b = wq @ b + quant_conv.bias.detach().float()
+        self._pc_out = ops.PackedConv([(w, self._block_out)], b, device=dev)
+        self._prepared_on = (dev, in_pad, quant_conv is not None)
+
+    def _run(self, x_nhwc):
+        """x_nhwc: fp16 [B, H, W, in_pad] → fp32 NCHW conv_out (∘ quant_conv) output."""
+        h = ops.conv2d(self._pc_in, x_nhwc)
+        for i_level in range(self.num_resolutions):
+            down = self.down[i_level]
+            for i_block in range(self.num_res_blocks):
+                h = down.block[i_block]._run(h)
+                if len(down.attn) > 0:
+                    h = down.attn[i_block]._run(h)
+            if i_level != self.num_resolutions - 1:
+                h = down.downsample._run(h)
+        h = self.mid.block_1._run(h)
+        h = self.mid.attn_1._run(h)
+        h = self.mid.block_2._run(h)
+        ha = ops.group_norm_apply(h, gn_stats(self.norm_out, h), silu=True)
+        return ops.conv2d(self._pc_out, ha, out_mode=ops.OUT_NCHW_F32)
+
+    @torch.no_grad()
     def forward(self, x):
-        raise NotImplementedError("sd_amd: VAE encode (img2img / training) is outside this round's hot path")
+        if not x.is_cuda:
+            raise TypeError("sd_amd.Encoder: HIP path only — move inputs to the GPU")
+        in_pad = (x.shape[1] + 7) // 8 * 8
+        if getattr(self, "_prepared_on", None) != (x.device, in_pad, False):
+            self._prepare(x.device, in_pad)
+        return self._run(ops.nchw_to_nhwc(x.float(), in_pad))
 
 
 class Decoder(nn.Module):

@@ -45,14 +45,24 @@ class Upsample(nn.Module):
 
 
 class Downsample(nn.Module):
-    """Encoder-side (asymmetric (0,1,0,1) pad + conv3x3 s2 p0, ``unet.py:52-71``): parameter holder;
-    the encoder is outside this round's hot path."""
+    """Encoder-side downsample (``unet.py:52-71``): F.pad(x, (0,1,0,1)) + conv3x3 s2 p0, run as one
+    implicit-GEMM conv with ``pad_end=1`` (the extra bottom/right zero row and column are taps
+    that fall outside the source, read as zeros — no padded copy)."""
 
     def __init__(self, in_channels, with_conv):
         super().__init__()
         self.with_conv = with_conv
+        self.in_channels = in_channels
         if with_conv:
             self.conv = nn.Conv2d(in_channels, in_channels, kernel_size=3, stride=2, padding=0)
+
+    def _prepare(self, dev):
+        if not self.with_conv:
+            raise NotImplementedError("sd_amd: avg-pool Downsample (with_conv=False) is not on the SD path")
+        self._pc = ops.PackedConv([(self.conv.weight, self.in_channels)], self.conv.bias, device=dev)
+
+    def _run(self, x):
+        return ops.conv2d(self._pc, x, stride=2, pad=0, pad_end=1)
 
 
 class ResnetBlock(nn.Module):

@@ -1,6 +1,9 @@
-"""Mirror of ``VAE/autoencoder.py`` — AutoEncoderKL (decode on the HIP path).
+"""Mirror of ``VAE/autoencoder.py`` — AutoEncoderKL (encode and decode on the HIP path).
 
 ``decode(z)`` = post_quant_conv (1x1) → Decoder (``autoencoder.py:126-132``).
+``encode(x)`` = Encoder → quant_conv (folded into the encoder's conv_out) →
+DiagonalGaussianDistribution (``autoencoder.py:114-123``); the encoder is packed on the
+first encode call.
 The 1x1 post_quant_conv runs as a GEMM whose output is zero-padded to 8
 channels (the NHWC kernels need 8-channel granularity); the decoder's conv_in
 consumes those 8 channels with zero weights on the padding.
@@ -15,6 +18,7 @@ import torch
 from torch import nn
 
 from .. import ops
+from ..Distribution.distribution import DiagonalGaussianDistribution
 from ..Encoder_Decoder.encoder import Decoder, Encoder
 
 
@@ -48,6 +52,7 @@ class AutoEncoderKL(nn.Module):
 
     def load_state_dict(self, *args, **kwargs):
         self._prepared_on = None
+        self.encoder._prepared_on = None
         return super().load_state_dict(*args, **kwargs)
 
     @torch.no_grad()
@@ -64,8 +69,16 @@ class AutoEncoderKL(nn.Module):
         self.decoder._prepared_on = (dev, self._zcp)
         self._prepared_on = dev
 
+    @torch.no_grad()
     def encode(self, x):
-        raise NotImplementedError("sd_amd: VAE encode (img2img / training) is outside this round's hot path")
+        """x: NCHW image [B, in_channels, H, W] (any float dtype) → DiagonalGaussianDistribution."""
+        if not x.is_cuda:
+            raise TypeError("sd_amd.AutoEncoderKL: HIP path only — move inputs to the GPU")
+        in_pad = (x.shape[1] + 7) // 8 * 8
+        if getattr(self.encoder, "_prepared_on", None) != (x.device, in_pad, True):
+            self.encoder._prepare(x.device, in_pad, quant_conv=self.quant_conv)
+        moments = self.encoder._run(ops.nchw_to_nhwc(x.float(), in_pad))
+        return DiagonalGaussianDistribution(moments)
 
     @torch.no_grad()
     def decode(self, z, pre_scale: float = 1.0):
@@ -79,8 +92,11 @@ class AutoEncoderKL(nn.Module):
         zq = ops.conv2d(self._pc_pq, zn)
         return self.decoder._run(zq)
 
+    @torch.no_grad()
     def forward(self, input, sample_posterior=True):
-        raise NotImplementedError("sd_amd: AutoEncoderKL.forward needs encode (outside this round's hot path)")
+        posterior = self.encode(input)
+        z = posterior.sample() if sample_posterior else posterior.mode()
+        return self.decode(z), posterior
 
 
 def instantiate_from_config(config):

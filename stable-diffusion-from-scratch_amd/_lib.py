@@ -20,7 +20,7 @@ fp = C.POINTER(C.c_float)
 class ConvSrc(C.Structure):
     _fields_ = [("src0", vp), ("src1", vp), ("c_split", i32), ("cin", i32), ("ld0", i32), ("ld1", i32),
                 ("h", i32), ("w", i32), ("ksize", i32), ("stride", i32), ("pad", i32), ("upsample", i32),
-                ("gn_scale", vp), ("gn_shift", vp), ("silu", i32)]
+                ("gn_scale", vp), ("gn_shift", vp), ("silu", i32), ("pad_end", i32)]
 
 
 class ConvArgs(C.Structure):
@@ -58,7 +58,7 @@ OUT_NHWC_F16, OUT_NCHW_F32, OUT_GEGLU_F16, OUT_ROWS_F32 = 0, 1, 2, 3
 
 EXPORTS = ["sdk_conv2d_plan", "sdk_conv2d", "sdk_group_norm_workspace", "sdk_group_norm_affine", "sdk_group_norm_apply", "sdk_layer_norm",
            "sdk_attention", "sdk_ddim_step", "sdk_ddpm_step", "sdk_timestep_embedding", "sdk_nchw_to_nhwc",
-           "sdk_last_error", "sdk_version", "sdk_kernel_name"]
+           "sdk_diag_gaussian_sample", "sdk_stochastic_encode", "sdk_last_error", "sdk_version", "sdk_kernel_name"]
 
 _lib = None
 
@@ -82,6 +82,8 @@ def lib():
     L.sdk_ddpm_step.argtypes = [vp, vp, vp, vp, i64, f32, f32, f32, vp]
     L.sdk_timestep_embedding.argtypes = [vp, vp, vp, i32, i32, vp]
     L.sdk_nchw_to_nhwc.argtypes = [vp, vp, i32, i32, i32, i32, f32, vp]
+    L.sdk_diag_gaussian_sample.argtypes = [vp, vp, vp, i32, i32, i32, f32, vp]
+    L.sdk_stochastic_encode.argtypes = [vp, vp, vp, i64, f32, f32, vp]
     L.sdk_last_error.restype = C.c_char_p
     L.sdk_kernel_name.restype = C.c_char_p
     L.sdk_kernel_name.argtypes = [i32]

@@ -1582,7 +1582,11 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
     if (g.ksize != 1 && g.ksize != 3) return fail(SDK_EINVAL, "conv2d: ksize must be 1 or 3");
     if ((g.gn_scale == nullptr) != (g.gn_shift == nullptr)) return fail(SDK_EINVAL, "conv2d: gn scale/shift pair");
     const int lh = g.upsample ? 2 * g.h : g.h, lw = g.upsample ? 2 * g.w : g.w;
-    const int eh = (lh + 2 * g.pad - g.ksize) / g.stride + 1, ew = (lw + 2 * g.pad - g.ksize) / g.stride + 1;
+    if (g.pad_end < 0 || g.pad_end > 2 || (g.pad_end && g.upsample))
+      return fail(SDK_EINVAL, "conv2d: pad_end must be 0..2 (no upsample)");
+    // zero padding is implicit (taps outside the source read zeros), so pad_end only widens the grid
+    const int eh = (lh + 2 * g.pad + g.pad_end - g.ksize) / g.stride + 1;
+    const int ew = (lw + 2 * g.pad + g.pad_end - g.ksize) / g.stride + 1;
     if (eh != a->ho || ew != a->wo) return fail(SDK_EINVAL, "conv2d: output size does not match source geometry");
     d.src0 = (const half_t*)g.src0; d.src1 = (const half_t*)g.src1;
     d.gscale = g.gn_scale; d.gshift = g.gn_shift;
@@ -1614,7 +1618,7 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
     // from one concat source, and a second segment that is a plain 1x1 over the output grid
     if ((double)a->batch * g.h * g.w * std::max(g.ld0, g.ld1) * 2 >= 2147483647.0) transform = true;
     if (g.c_split < g.cin && g.c_split % BK) transform = true;
-    if (s == 1 && (g.ksize != 1 || g.stride != 1 || g.pad != 0 || g.upsample || g.h != a->ho || g.w != a->wo))
+    if (s == 1 && (g.ksize != 1 || g.stride != 1 || g.pad != 0 || g.pad_end || g.upsample || g.h != a->ho || g.w != a->wo))
       transform = true;
   }
   if ((double)((a->cout + 127) / 128 * 128) * a->k_total * 2 >= 2147483647.0) transform = true;

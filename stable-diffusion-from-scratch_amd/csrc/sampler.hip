@@ -116,10 +116,57 @@ __global__ void __launch_bounds__(256) nchw_to_nhwc_kernel(const float* x, half_
   }
 }
 
+// grid-stride over the latent elements; moments = [mean | logvar] along channels (NCHW)
+__global__ void __launch_bounds__(256) diag_gauss_kernel(const float* moments, const float* noise, float* z,
+                                                         int channels, int hw, int64_t n, float scale) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t per_img = (int64_t)channels * hw;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t b = i / per_img, r = i - b * per_img;
+    const float mean = moments[b * 2 * per_img + r];
+    float v = mean;
+    if (noise) {
+      const float lv = fminf(fmaxf(moments[b * 2 * per_img + per_img + r], -30.f), 20.f);
+      const float sd = expf(0.5f * lv);
+      v = mean + sd * noise[i];
+    }
+    z[i] = scale * v;
+  }
+}
+
+__global__ void __launch_bounds__(256) stochastic_encode_kernel(const float* x0, const float* noise, float* out,
+                                                                int64_t n, float sa, float s1ma) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float t0 = sa * x0[i];
+    const float t1 = s1ma * noise[i];
+    out[i] = t0 + t1;
+  }
+}
+
 }  // namespace
 }  // namespace sdk
 
 using namespace sdk;
+
+extern "C" int sdk_diag_gaussian_sample(const float* moments, const float* noise, float* z, int32_t batch,
+                                        int32_t channels, int32_t hw, float scale, sdk_stream_t stream) {
+  if (!moments || !z || batch <= 0 || channels <= 0 || hw <= 0) return fail(SDK_EINVAL, "diag_gaussian_sample: bad args");
+  const int64_t n = (int64_t)batch * channels * hw;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 2048);
+  hipLaunchKernelGGL(diag_gauss_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, moments, noise, z, channels,
+                     hw, n, scale);
+  return check_launch("diag_gaussian_sample");
+}
+
+extern "C" int sdk_stochastic_encode(const float* x0, const float* noise, float* out, int64_t n, float sqrt_a,
+                                     float sqrt_1ma, sdk_stream_t stream) {
+  if (!x0 || !noise || !out || n <= 0) return fail(SDK_EINVAL, "stochastic_encode: bad args");
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 2048);
+  hipLaunchKernelGGL(stochastic_encode_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x0, noise, out, n,
+                     sqrt_a, sqrt_1ma);
+  return check_launch("stochastic_encode");
+}
 
 extern "C" int sdk_ddim_step(const sdk_ddim_args* a, sdk_stream_t stream) {
   if (!a || !a->x || !a->e || !a->x_prev) return fail(SDK_EINVAL, "ddim_step: null pointer");

@@ -263,10 +263,11 @@ class _Autotune:
 AUTOTUNE = _Autotune()
 
 
-def conv2d(pc: PackedConv, x, *, ksize=None, stride=1, pad=None, upsample=False, gn=None, silu=False,
+def conv2d(pc: PackedConv, x, *, ksize=None, stride=1, pad=None, pad_end=0, upsample=False, gn=None, silu=False,
            seg2=None, bias=True, row_bias=None, residual=None, out_mode=OUT_NHWC_F16, out=None,
            variant=None, split_k=None):
     """Run the implicit-GEMM conv.  ``seg2`` = (x2, gn2, silu2) adds a fused 1x1 K segment.
+    ``pad_end`` adds zero rows/cols after the source (asymmetric (0,1,0,1) padding).
     ``row_bias`` = (fp32 tensor [B, ld], column offset) — the per-(batch, channel) add.
     ``variant`` / ``split_k`` force a kernel configuration (benchmarks; default: planner
     or autotuner)."""
@@ -275,9 +276,10 @@ def conv2d(pc: PackedConv, x, *, ksize=None, stride=1, pad=None, upsample=False,
     if pad is None:
         pad = k0 // 2
     B, H, W = _fill_src(a.seg[0], x, k0, stride, pad, upsample, gn, silu)
+    a.seg[0].pad_end = pad_end
     lh, lw = (2 * H, 2 * W) if upsample else (H, W)
-    Ho = (lh + 2 * pad - k0) // stride + 1
-    Wo = (lw + 2 * pad - k0) // stride + 1
+    Ho = (lh + 2 * pad + pad_end - k0) // stride + 1
+    Wo = (lw + 2 * pad + pad_end - k0) // stride + 1
     a.nseg = 1
     if seg2 is not None:
         x2, gn2, silu2 = seg2
@@ -492,6 +494,31 @@ def ddim_step(x, e, sc: dict, noise=None, e_uncond=None, guidance=1.0, v_param=N
         a.v_sqrt_a, a.v_sqrt_1ma = float(v_param[0]), float(v_param[1])
     check(lib().sdk_ddim_step(C.byref(a), _stream()), "ddim_step")
     return xp, p0
+
+
+def diag_gaussian_sample(moments: torch.Tensor, noise=None, scale: float = 1.0, out=None):
+    """moments NCHW fp32 [B, 2C, H, W] -> scale * (mean + std * noise) (or scale * mean) [B, C, H, W]."""
+    _need_cuda(moments, "diag_gaussian_sample", torch.float32)
+    B, C2, H, W = moments.shape
+    moments = moments.contiguous()
+    if noise is not None:
+        _need_cuda(noise, "diag_gaussian_sample noise", torch.float32)
+        noise = noise.contiguous()
+    z = out if out is not None else torch.empty(B, C2 // 2, H, W, dtype=torch.float32, device=moments.device)
+    check(lib().sdk_diag_gaussian_sample(_ptr(moments), _ptr(noise), _ptr(z), B, C2 // 2, H * W, float(scale),
+                                         _stream()), "diag_gaussian_sample")
+    return z
+
+
+def stochastic_encode(x0: torch.Tensor, noise: torch.Tensor, sqrt_a: float, sqrt_1ma: float, out=None):
+    """sqrt_a * x0 + sqrt_1ma * noise, fp32, bit-identical to the reference's CPU expression."""
+    _need_cuda(x0, "stochastic_encode", torch.float32)
+    _need_cuda(noise, "stochastic_encode noise", torch.float32)
+    x0, noise = x0.contiguous(), noise.contiguous()
+    y = out if out is not None else torch.empty_like(x0)
+    check(lib().sdk_stochastic_encode(_ptr(x0), _ptr(noise), _ptr(y), x0.numel(), float(sqrt_a), float(sqrt_1ma),
+                                      _stream()), "stochastic_encode")
+    return y
 
 
 def ddpm_step(x, eps, noise, inv_sqrt_alpha, coef, sigma, out=None):

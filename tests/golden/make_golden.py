@@ -280,6 +280,69 @@ def gen_vae():
                         cfg=np.frombuffer(json.dumps(TINY_VAE).encode(), dtype=np.uint8))
 
 
+def gen_img2img(fake):
+    """SURVEY §8(f) rank 2 — img2img: AutoEncoderKL.encode → posterior (moments, a recorded-noise
+    sample; VAE/autoencoder.py:114-123, Distribution/distribution.py:31-50), DDIMSampler.stochastic_encode
+    at uniform and per-sample DDIM indices (DDIM/ddim.py:207-220) and DDIMSampler.decode from t_start
+    with a deterministic stub ε-model (DDIM/ddim.py:222-240)."""
+    with quiet():
+        import Unet.unet as uu
+        import Encoder_Decoder.encoder as ee
+        silu = lambda x: x * torch.sigmoid(x)        # SURVEY §8(c) item 6: no fp16 cast
+        uu.nonlinearity = silu
+        ee.nonlinearity = silu
+        from VAE.autoencoder import AutoEncoderKL
+        vae = AutoEncoderKL(ddconfig=dict(TINY_VAE), embed_dim=4, lossconfig={"target": "torch.nn.Identity"})
+    reinit_(vae, 13)
+    vae.eval()
+    g = torch.Generator().manual_seed(14)
+    x = torch.rand(2, 3, 32, 32, generator=g) * 2.0 - 1.0
+    real_randn = torch.randn
+    rec = []
+
+    def rec_randn(*shape, **kw):
+        t = real_randn(*shape, generator=g)
+        rec.append(t.clone())
+        return t
+
+    with quiet(), torch.no_grad():
+        post = vae.encode(x)
+        torch.randn = rec_randn
+        try:
+            smp = post.sample()
+        finally:
+            torch.randn = real_randn
+    out = {"x": x.numpy(), "moments": post.parameters.numpy(), "post_noise": rec[0].numpy(),
+           "post_sample": smp.numpy(), "post_mode": post.mean.numpy(), "seed": np.int64(13),
+           "cfg": np.frombuffer(json.dumps(TINY_VAE).encode(), dtype=np.uint8)}
+    out.update(sd_keys(vae))
+
+    ddim_mod = make_ddim_sampler(fake)
+
+    class M:
+        num_timesteps = 1000
+        alphas_cumprod = fake.alphas_cumprod
+        alphas_cumprod_prev = fake.alphas_cumprod_prev
+        betas = fake.betas
+        device = torch.device("cpu")
+        parameterization = "eps"
+
+        def apply_model(self, x, t, c):
+            return 0.5 * x + 0.01 * t.float()[:, None, None, None]
+
+    s = ddim_mod.DDIMSampler(M())
+    with quiet():
+        s.make_schedule(50, ddim_eta=0.0, verbose=False)
+    z0 = 0.18215 * smp
+    nz = torch.randn(z0.shape, generator=g)
+    out["z0"], out["enc_noise"] = z0.numpy(), nz.numpy()
+    with quiet(), torch.no_grad():
+        out["enc_t30"] = s.stochastic_encode(z0, torch.full((2,), 30, dtype=torch.long), noise=nz).numpy()
+        out["enc_t10_40"] = s.stochastic_encode(z0, torch.tensor([10, 40]), noise=nz).numpy()
+        out["dec_t5"] = s.decode(torch.from_numpy(out["enc_t30"]), None, 5).numpy()
+    np.savez_compressed(os.path.join(OUT, "img2img.npz"), **out)
+
+
 def gen_ddpm():
     """C1 pipeline: DDPMPipeline tables + a 10-step sampling run with a recorded-ε
     stub model and recorded noise (DDPM/ddpm.py:17-89)."""
@@ -321,6 +384,7 @@ def main():
     gen_unet("unet_tiny_uncond", TINY_UNET_UNCOND, 5, with_ctx=False)
     gen_unet("unet_tiny_headch", TINY_UNET_HC, 9, with_ctx=True)
     gen_vae()
+    gen_img2img(fake)
     gen_ddpm()
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):

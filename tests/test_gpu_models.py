@@ -120,3 +120,115 @@ def test_full_vae_decode_vs_oracle(sdk):
     err = rel_l2(dec, ref)
     print(f"VAE rel-L2 {err:.3e}")
     assert err < 2e-2
+
+
+# ---------------------------------------------------------------- img2img
+def _tiny_img2img_vae(z):
+    from sd_amd.VAE.autoencoder import AutoEncoderKL
+    vae = AutoEncoderKL(ddconfig=cfg_of(z), embed_dim=4)
+    vae.load_state_dict(weights_of(z))
+    return vae
+
+
+def test_tiny_vae_encode_vs_reference(sdk):
+    """Encoder (asymmetric-pad Downsample, mid attention) + quant_conv vs the reference's
+    posterior parameters; posterior sample with the reference's recorded noise; mode."""
+    z = load("img2img")
+    vae = _tiny_img2img_vae(z)
+    post = vae.encode(torch.from_numpy(z["x"]).to(DEV))
+    assert post.parameters.shape == z["moments"].shape
+    assert rel_l2(post.parameters, torch.from_numpy(z["moments"])) < 1e-2
+    smp = post.sample(noise=torch.from_numpy(z["post_noise"]).to(DEV))
+    assert rel_l2(smp, torch.from_numpy(z["post_sample"])) < 1e-2
+    assert rel_l2(post.mode(), torch.from_numpy(z["post_mode"])) < 1e-2
+    # exact posterior arithmetic on identical moments (tolerance: device expf vs CPU exp, 1e-6)
+    from oracle.vae_ref import posterior_sample
+    from sd_amd import ops
+    m = torch.from_numpy(z["moments"])
+    got = ops.diag_gaussian_sample(m.to(DEV), torch.from_numpy(z["post_noise"]).to(DEV), 0.18215)
+    ref = posterior_sample(m, torch.from_numpy(z["post_noise"]), 0.18215)
+    assert torch.allclose(got.cpu(), ref, rtol=1e-6, atol=1e-6)
+
+
+def test_stochastic_encode_bitexact(sdk):
+    """DDIMSampler.stochastic_encode at a uniform and per-sample DDIM index: bit-exact vs the reference."""
+    from sd_amd.DDIM.ddim import DDIMSampler
+    from sd_amd.DDIM.diffusion_modules import register_schedule
+    z = load("img2img")
+    sch = register_schedule(1000, 0.00085, 0.012)
+
+    class LD:
+        num_timesteps = 1000
+        alphas_cumprod = sch["alphas_cumprod"]
+        device = torch.device(DEV)
+
+    s = DDIMSampler(LD())
+    s.make_schedule(50, ddim_eta=0.0, verbose=False)
+    z0, nz = torch.from_numpy(z["z0"]).to(DEV), torch.from_numpy(z["enc_noise"]).to(DEV)
+    a = s.stochastic_encode(z0, torch.full((2,), 30, dtype=torch.long), noise=nz).cpu().numpy()
+    assert np.array_equal(a, z["enc_t30"])
+    b = s.stochastic_encode(z0, torch.tensor([10, 40]), noise=nz).cpu().numpy()
+    assert np.array_equal(b, z["enc_t10_40"])
+
+
+def test_ddim_decode_from_t_start_bitexact(sdk):
+    """DDIMSampler.decode (img2img denoising from t_start=5) with the reference's stub ε-model:
+    timestep/index bookkeeping and the fused update bit-exact vs the reference."""
+    from sd_amd.DDIM.ddim import DDIMSampler
+    from sd_amd.DDIM.diffusion_modules import register_schedule
+    z = load("img2img")
+    sch = register_schedule(1000, 0.00085, 0.012)
+
+    class LD:
+        num_timesteps = 1000
+        alphas_cumprod = sch["alphas_cumprod"]
+        device = torch.device(DEV)
+        parameterization = "eps"
+
+        def apply_model(self, x, t, c):
+            return 0.5 * x + 0.01 * t.float()[:, None, None, None]
+
+    s = DDIMSampler(LD())
+    s.make_schedule(50, ddim_eta=0.0, verbose=False)
+    out = s.decode(torch.from_numpy(z["enc_t30"]).to(DEV), None, 5).cpu().numpy()
+    assert np.array_equal(out, z["dec_t5"])
+
+
+def test_downsample_asymmetric_pad_vs_torch(sdk):
+    """Downsample: F.pad(0,1,0,1) + conv3x3 s2 p0 as one pad_end conv, odd and even sizes."""
+    import torch.nn.functional as F
+    from sd_amd.Unet.unet import Downsample
+    for hw in (16, 17, 64):
+        m = Downsample(128, True)
+        torch.nn.init.normal_(m.conv.weight, std=0.05)
+        m._prepare(torch.device(DEV))
+        g = torch.Generator().manual_seed(hw)
+        x = torch.randn(2, 128, hw, hw, generator=g)
+        from sd_amd import ops
+        y = m._run(ops.nchw_to_nhwc(x.to(DEV), 128)).float().permute(0, 3, 1, 2).cpu()
+        ref = F.conv2d(F.pad(x, (0, 1, 0, 1)), m.conv.weight.detach(), m.conv.bias.detach(), stride=2)
+        assert y.shape == ref.shape, (hw, y.shape, ref.shape)
+        assert rel_l2(y, ref) < 3e-3
+
+
+def test_full_vae_encode_vs_oracle(sdk):
+    """SD VAE encoder (ch 128, mult [1,2,4,4]) at 512² → 64² moments, B=1 vs the fp32 CPU oracle."""
+    from oracle.vae_ref import autoencoder_moments
+    from sd_amd.VAE.autoencoder import AutoEncoderKL
+    dd = dict(double_z=True, z_channels=4, resolution=256, in_channels=3, out_ch=3, ch=128, ch_mult=[1, 2, 4, 4],
+              num_res_blocks=2, attn_resolutions=[], dropout=0.0)
+    with torch.device("meta"):
+        vae = AutoEncoderKL(ddconfig=dd, embed_dim=4)
+    ks = [(k, tuple(v.shape)) for k, v in vae.state_dict().items()]
+    sd = {k: torch.from_numpy(v) for k, v in synth_weights(ks, 78).items()}
+    vae = AutoEncoderKL(ddconfig=dd, embed_dim=4)
+    vae.load_state_dict(sd)
+    g = torch.Generator().manual_seed(4)
+    x = torch.rand(1, 3, 512, 512, generator=g) * 2 - 1
+    post = vae.encode(x.to(DEV))
+    torch.set_num_threads(16)
+    ref = autoencoder_moments(sd, dd, x)
+    err = rel_l2(post.parameters, ref)
+    print(f"VAE encode rel-L2 {err:.3e}")
+    assert post.parameters.shape == (1, 8, 64, 64)
+    assert err < 2e-2

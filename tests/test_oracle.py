@@ -102,3 +102,39 @@ def test_ddpm_c1_pipeline():
         sc = sch.ddpm_step_scalars(tab, t)
         img = sch.ddpm_step(img, eps, sc, noises.pop(0) if t > 0 else None)
     assert np.max(np.abs(img - z["out"])) <= 1e-5 * max(1.0, np.abs(z["out"]).max())
+
+
+# ---------------------------------------------------------------- img2img
+def test_vae_encode_moments():
+    z = load("img2img")
+    cfg, sd = cfg_of(z), weights_of(z)
+    m = vae_ref.autoencoder_moments(sd, cfg, torch.from_numpy(z["x"]))
+    ref = z["moments"]
+    assert m.shape == ref.shape
+    assert np.max(np.abs(m.numpy() - ref)) <= 1e-4 * max(1.0, np.abs(ref).max())
+
+
+def test_posterior_sample_and_mode():
+    z = load("img2img")
+    m = torch.from_numpy(z["moments"])
+    s = vae_ref.posterior_sample(m, torch.from_numpy(z["post_noise"]))
+    np.testing.assert_allclose(s.numpy(), z["post_sample"], rtol=1e-6, atol=1e-6)
+    assert np.array_equal(vae_ref.posterior_sample(m).numpy(), z["post_mode"])
+
+
+def test_stochastic_encode_bitexact():
+    z = load("img2img")
+    tab = sch.ddim_tables(50, 0.0)
+    got = sch.stochastic_encode(z["z0"], z["enc_noise"], tab, 30)
+    assert np.array_equal(got, z["enc_t30"])
+    per = np.stack([sch.stochastic_encode(z["z0"][i], z["enc_noise"][i], tab, t) for i, t in enumerate((10, 40))])
+    assert np.array_equal(per, z["enc_t10_40"])
+
+
+def test_ddim_decode_from_t_start_bitexact():
+    z = load("img2img")
+    tab = sch.ddim_tables(50, 0.0)
+    stub = lambda x, t: (np.float32(0.5) * x + np.float32(0.01) * t.astype(np.float32)[:, None, None, None]
+                         ).astype(np.float32)
+    out = sch.ddim_decode(z["enc_t30"], stub, tab, 5)
+    assert np.array_equal(out, z["dec_t5"]), np.max(np.abs(out - z["dec_t5"]))
