@@ -97,7 +97,13 @@ typedef struct {
   float* workspace;        /* split-K fp32 partials */
   int64_t workspace_bytes;
   int32_t variant_hint;    /* 0 = choose; 1 + variant id forces a tile configuration (autotuning) */
+  int32_t act;             /* enum sdk_conv_act: applied after bias / row_bias, before the residual */
 } sdk_conv_args;
+
+enum sdk_conv_act {
+  SDK_ACT_NONE = 0,
+  SDK_ACT_QUICK_GELU = 1   /* x * sigmoid(1.702 x): CLIP MLP fc1 (transformers QuickGELUActivation) */
+};
 
 typedef struct {
   int32_t split_k;
@@ -156,6 +162,7 @@ typedef struct {
   int32_t q_ld, k_ld, v_ld, o_ld;
   int32_t batch, heads, nq, nk, head_dim;
   float scale;
+  int32_t causal;          /* 1: key j is masked for query i when j > i (CLIP text encoder) */
 } sdk_attention_args;
 
 int sdk_attention(const sdk_attention_args* a, sdk_stream_t stream);
@@ -207,6 +214,14 @@ int sdk_diag_gaussian_sample(const float* moments, const float* noise, float* z,
  * bit-identical to torch's CPU evaluation of the reference expression. */
 int sdk_stochastic_encode(const float* x0, const float* noise, float* out, int64_t n, float sqrt_a,
                           float sqrt_1ma, sdk_stream_t stream);
+
+/* Token + position embedding of the CLIP text transformer (transformers CLIPTextEmbeddings,
+ * called by FrozenCLIPEmbedder.forward, clip_encoder/modules.py:241-256):
+ * out[b][t][:] = fp16(tok[ids[b][t]][:] + pos[t][:]), fp32 tables [vocab][dim] / [>= seq][dim].
+ * Ids outside [0, vocab) are an error (reported through sdk_last_error after the launch
+ * is skipped: the ids are checked on the host by the caller). */
+int sdk_token_embedding(const int64_t* ids, const float* tok, const float* pos, void* out, int32_t batch,
+                        int32_t seq, int32_t dim, sdk_stream_t stream);
 
 /* ---------------------------------------------------------------- introspection */
 const char* sdk_last_error(void);

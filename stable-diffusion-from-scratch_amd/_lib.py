@@ -27,7 +27,8 @@ class ConvArgs(C.Structure):
     _fields_ = [("batch", i32), ("ho", i32), ("wo", i32), ("cout", i32), ("nseg", i32), ("seg", ConvSrc * 2),
                 ("weight", vp), ("k_total", i32), ("bias", vp), ("row_bias", vp), ("row_bias_ld", i32),
                 ("residual", vp), ("res_ld", i32), ("out", vp), ("out_ld", i32), ("out_mode", i32),
-                ("split_k", i32), ("workspace", vp), ("workspace_bytes", i64), ("variant_hint", i32)]
+                ("split_k", i32), ("workspace", vp), ("workspace_bytes", i64), ("variant_hint", i32),
+                ("act", i32)]
 
 
 class ConvPlanInfo(C.Structure):
@@ -44,7 +45,7 @@ class GroupNormArgs(C.Structure):
 class AttentionArgs(C.Structure):
     _fields_ = [("q", vp), ("k", vp), ("v", vp), ("o", vp), ("q_ld", i32), ("k_ld", i32), ("v_ld", i32),
                 ("o_ld", i32), ("batch", i32), ("heads", i32), ("nq", i32), ("nk", i32), ("head_dim", i32),
-                ("scale", f32)]
+                ("scale", f32), ("causal", i32)]
 
 
 class DdimArgs(C.Structure):
@@ -55,10 +56,11 @@ class DdimArgs(C.Structure):
 
 
 OUT_NHWC_F16, OUT_NCHW_F32, OUT_GEGLU_F16, OUT_ROWS_F32 = 0, 1, 2, 3
+ACT_NONE, ACT_QUICK_GELU = 0, 1
 
 EXPORTS = ["sdk_conv2d_plan", "sdk_conv2d", "sdk_group_norm_workspace", "sdk_group_norm_affine", "sdk_group_norm_apply", "sdk_layer_norm",
            "sdk_attention", "sdk_ddim_step", "sdk_ddpm_step", "sdk_timestep_embedding", "sdk_nchw_to_nhwc",
-           "sdk_diag_gaussian_sample", "sdk_stochastic_encode", "sdk_last_error", "sdk_version", "sdk_kernel_name"]
+           "sdk_diag_gaussian_sample", "sdk_stochastic_encode", "sdk_token_embedding", "sdk_last_error", "sdk_version", "sdk_kernel_name"]
 
 _lib = None
 
@@ -84,6 +86,7 @@ def lib():
     L.sdk_nchw_to_nhwc.argtypes = [vp, vp, i32, i32, i32, i32, f32, vp]
     L.sdk_diag_gaussian_sample.argtypes = [vp, vp, vp, i32, i32, i32, f32, vp]
     L.sdk_stochastic_encode.argtypes = [vp, vp, vp, i64, f32, f32, vp]
+    L.sdk_token_embedding.argtypes = [vp, vp, vp, vp, i32, i32, i32, vp]
     L.sdk_last_error.restype = C.c_char_p
     L.sdk_kernel_name.restype = C.c_char_p
     L.sdk_kernel_name.argtypes = [i32]

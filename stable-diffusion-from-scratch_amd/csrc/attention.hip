@@ -42,6 +42,7 @@ struct AttnParams {
   int q_ld, k_ld, v_ld, o_ld;
   int batch, heads, nq, nk, d;
   float c;              // scale * log2(e)
+  int causal;           // mask key > query
 };
 
 typedef __fp16 fp16x4_t __attribute__((ext_vector_type(4)));
@@ -149,7 +150,11 @@ __global__ void __launch_bounds__(NW * 64, QB == 2 ? 1 : 2) attn_fwd_kernel(Attn
   f16v negm[QB];
 #pragma unroll
   for (int qb = 0; qb < QB; ++qb) { m_run[qb] = 0.f; l_run[qb] = 0.f; negm[qb] = f16v{}; }
-  const int ntiles = (p.nk + KT - 1) / KT;
+  int ntiles = (p.nk + KT - 1) / KT;
+  if (p.causal) {   // tiles past the workgroup's last query row hold only masked keys
+    const int qlast = min(p.nq, (int)(blockIdx.x + 1) * (32 * QB * NW)) - 1;
+    ntiles = min(ntiles, qlast / KT + 1);
+  }
 
   // transposed-read addressing for the V^T operand (32x32x16, A side):
   // group g = lane>>4 reads keys 16ks + 4*(g>>1) + 8*hi .. +3, columns 32*db + 16*(g&1) .. +15;
@@ -190,13 +195,14 @@ __global__ void __launch_bounds__(NW * 64, QB == 2 ? 1 : 2) attn_fwd_kernel(Attn
     h8 pf[QB][4];
 #pragma unroll
     for (int qb = 0; qb < QB; ++qb) {
-      if (key0 + KT > p.nk) {           // ragged last tile only
+      const int qrow = q0 + qb * 32 + fr;
+      if (key0 + KT > p.nk || (p.causal && key0 + KT - 1 > q0 + qb * 32)) {   // ragged / diagonal tiles only
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
-            if (key >= p.nk) s[qb][kb][r] = -1e30f;
+            if (key >= p.nk || (p.causal && key > qrow)) s[qb][kb][r] = -1e30f;
           }
       }
       float mt = fmaxf(s[qb][0][0], s[qb][0][1]);
@@ -324,7 +330,7 @@ extern "C" int sdk_attention(const sdk_attention_args* a, sdk_stream_t stream) {
     return fail(SDK_EINVAL, "attention: one image's K/V exceeds the 2 GiB buffer range");
   AttnParams p{(const half_t*)a->q, (const half_t*)a->k, (const half_t*)a->v, (half_t*)a->o,
                a->q_ld, a->k_ld, a->v_ld, a->o_ld, a->batch, a->heads, a->nq, a->nk, a->head_dim,
-               a->scale * 1.4426950408889634f};
+               a->scale * 1.4426950408889634f, a->causal ? 1 : 0};
   hipStream_t s = (hipStream_t)stream;
   const int d = a->head_dim;
   // one 32-row query block per wave at 3-4 waves per SIMD; SDK_ATTN_QB=2 selects two blocks per

@@ -59,7 +59,14 @@ struct Params {
   int split, kt_per_split;
   int tiles_m, tiles_n;
   int variant;          // 0: register-staged 128x128 (A transforms); 2/3/4: LDS-DMA 256x256 / 256x128 / 128x128
+  int act;              // epilogue activation after bias / embedding, before the residual (sdk_conv_act)
 };
+
+// epilogue activation (CLIP's quick_gelu x*sigmoid(1.702x), transformers activations.py QuickGELUActivation)
+__device__ __forceinline__ float act_fn(int act, float x) {
+  if (act == SDK_ACT_QUICK_GELU) return x * __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * x));
+  return x;
+}
 
 __device__ __forceinline__ int swz(int row, int chunk) {   // element offset inside a [128][64] tile
   return row * BK + ((chunk ^ ((row >> 1) & 7)) << 3);
@@ -227,7 +234,7 @@ __device__ __forceinline__ void epilogue(const Params& p, f16v (&acc)[FM][FN], h
             const int m = min(m0 + rl, p.M - 1);
             v += p.row_bias[(size_t)(m / p.hw_out) * p.rb_ld + n];
           }
-          smem[rl * CLD + n_w + j * 32 + fr] = (half_t)v;
+          smem[rl * CLD + n_w + j * 32 + fr] = (half_t)act_fn(p.act, v);
         }
       }
     }
@@ -261,6 +268,7 @@ __device__ __forceinline__ void epilogue(const Params& p, f16v (&acc)[FM][FN], h
         const int b = m / p.hw_out;
         float v = acc[i][j][r] + bn[j];
         if (p.row_bias) v += p.row_bias[(size_t)b * p.rb_ld + n];
+        v = act_fn(p.act, v);
         if (p.res) v += (float)p.res[(size_t)m * p.res_ld + n];
         float* out = reinterpret_cast<float*>(p.out);
         if (mode == SDK_OUT_NCHW_F32)
@@ -460,7 +468,7 @@ __device__ __forceinline__ void epilogue_direct(const Params& p, f16v (&acc)[FM]
           }
           h4 o;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) o[q] = (half_t)v[q];
+          for (int q = 0; q < 4; ++q) o[q] = (half_t)act_fn(p.act, v[q]);
           if (p.res) {
             const h4 rr = *reinterpret_cast<const h4*>(p.res + (size_t)m * p.res_ld + n);
 #pragma unroll
@@ -484,6 +492,7 @@ __device__ __forceinline__ void epilogue_direct(const Params& p, f16v (&acc)[FM]
           float x = acc[i][j][4 * g + q];
           if (p.bias) x += p.bias[n + q];
           if (p.row_bias) x += p.row_bias[(size_t)b * p.rb_ld + n + q];
+          x = act_fn(p.act, x);
           if (p.res) x += (float)p.res[(size_t)m * p.res_ld + n + q];
           if (mode == SDK_OUT_NCHW_F32)
             out[((size_t)b * p.N + n + q) * p.hw_out + (m - b * p.hw_out)] = x;
@@ -591,7 +600,7 @@ __device__ __forceinline__ void epilogue_lds(const Params& p, f16v (&acc)[FM][FN
           }
           h4 o;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) o[q] = (half_t)v[q];
+          for (int q = 0; q < 4; ++q) o[q] = (half_t)act_fn(p.act, v[q]);
           *reinterpret_cast<h4*>(wbuf + fr * EPI_RS + jj * 32 + 8 * g + 4 * fh) = o;
         }
       }
@@ -686,7 +695,7 @@ __device__ __forceinline__ void epi16_group(const Params& p, const f4* a, int mt
     }
     h4 o;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) o[q] = (half_t)v[q];
+    for (int q = 0; q < 4; ++q) o[q] = (half_t)act_fn(p.act, v[q]);
     *reinterpret_cast<h4*>(wbuf + px * EPG_RS + 16 * j + 4 * cg) = o;
   }
   constexpr int LPR = NB * 2, RPI = 64 / LPR;       // lanes per row, rows per instruction
@@ -746,6 +755,7 @@ __device__ __forceinline__ void epilogue16_tile_direct(const Params& p, f4 (&acc
         float x = acc[i][j][q];
         if (p.bias) x += p.bias[n + q];
         if (p.row_bias) x += p.row_bias[(size_t)b * p.rb_ld + n + q];
+        x = act_fn(p.act, x);
         if (p.res) x += (float)p.res[(size_t)m * p.res_ld + n + q];
         if (p.out_mode == SDK_OUT_NCHW_F32)
           out[((size_t)b * p.N + n + q) * p.hw_out + (m - b * p.hw_out)] = x;
@@ -1162,7 +1172,7 @@ __device__ __forceinline__ void epilogue16_lds(const Params& p, f4 (&acc)[4][2][
         }
         h4 o;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) o[q] = (half_t)v[q];
+        for (int q = 0; q < 4; ++q) o[q] = (half_t)act_fn(p.act, v[q]);
         *reinterpret_cast<h4*>(wbuf + px * EPI16_RS + 32 * b + 16 * j + 4 * cg) = o;
       }
     // read back: 16 pixel rows x 64 channels = 8 lanes x 16 B per row, 8 rows per instruction
@@ -1208,6 +1218,7 @@ __device__ __forceinline__ void epilogue16_direct(const Params& p, f4 (&acc)[4][
           float x = acc[i][b2][j][q];
           if (p.bias) x += p.bias[n + q];
           if (p.row_bias) x += p.row_bias[(size_t)b * p.rb_ld + n + q];
+          x = act_fn(p.act, x);
           if (p.res) x += (float)p.res[(size_t)m * p.res_ld + n + q];
           if (p.out_mode == SDK_OUT_NCHW_F32)
             out[((size_t)b * p.N + n + q) * p.hw_out + (m - b * p.hw_out)] = x;
@@ -1518,6 +1529,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(Params p) {
     for (int j = 0; j < 8; ++j) {
       if (p.bias) v[j] += p.bias[n + j];
       if (p.row_bias) v[j] += p.row_bias[(size_t)b * p.rb_ld + n + j];
+      v[j] = act_fn(p.act, v[j]);
     }
     if (p.out_mode == SDK_OUT_NHWC_F16) {
       h8 o;
@@ -1565,6 +1577,10 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
     return fail(SDK_EINVAL, "conv2d: empty output shape");
   if (!a->weight || !a->out) return fail(SDK_EINVAL, "conv2d: null weight/out");
   p = Params{};
+  if (a->act != SDK_ACT_NONE && a->act != SDK_ACT_QUICK_GELU) return fail(SDK_EINVAL, "conv2d: unknown act");
+  if (a->act != SDK_ACT_NONE && a->out_mode == SDK_OUT_GEGLU_F16)
+    return fail(SDK_EINVAL, "conv2d: act does not combine with the GEGLU epilogue");
+  p.act = a->act;
   p.batch = a->batch; p.ho = a->ho; p.wo = a->wo; p.hw_out = a->ho * a->wo;
   p.M = a->batch * p.hw_out;
   p.N = a->cout;

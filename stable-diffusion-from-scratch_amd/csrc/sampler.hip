@@ -144,10 +144,33 @@ __global__ void __launch_bounds__(256) stochastic_encode_kernel(const float* x0,
   }
 }
 
+// one block per token row: 8 channels per thread, fp32 sum rounded once to fp16
+__global__ void __launch_bounds__(128) token_embedding_kernel(const int64_t* ids, const float* tok, const float* pos,
+                                                              half_t* out, int seq, int dim) {
+  const int row = blockIdx.x, t = row % seq;
+  const int64_t id = ids[row];
+  for (int c = threadIdx.x * 4; c < dim; c += blockDim.x * 4) {
+    const f4 a = *reinterpret_cast<const f4*>(tok + id * dim + c);
+    const f4 b = *reinterpret_cast<const f4*>(pos + (int64_t)t * dim + c);
+    h4 o;
+    for (int j = 0; j < 4; ++j) o[j] = (half_t)(a[j] + b[j]);
+    *reinterpret_cast<h4*>(out + (int64_t)row * dim + c) = o;
+  }
+}
+
 }  // namespace
 }  // namespace sdk
 
 using namespace sdk;
+
+extern "C" int sdk_token_embedding(const int64_t* ids, const float* tok, const float* pos, void* out, int32_t batch,
+                                   int32_t seq, int32_t dim, sdk_stream_t stream) {
+  if (!ids || !tok || !pos || !out || batch <= 0 || seq <= 0 || dim <= 0 || dim % 4)
+    return fail(SDK_EINVAL, "token_embedding: bad args (dim must be a multiple of 4)");
+  hipLaunchKernelGGL(token_embedding_kernel, dim3(batch * seq), dim3(128), 0, (hipStream_t)stream, ids, tok, pos,
+                     (half_t*)out, seq, dim);
+  return check_launch("token_embedding");
+}
 
 extern "C" int sdk_diag_gaussian_sample(const float* moments, const float* noise, float* z, int32_t batch,
                                         int32_t channels, int32_t hw, float scale, sdk_stream_t stream) {

@@ -15,8 +15,8 @@ import math
 import torch
 
 from . import _lib
-from ._lib import (AttentionArgs, ConvArgs, ConvPlanInfo, DdimArgs, GroupNormArgs, OUT_GEGLU_F16, OUT_NCHW_F32,
-                   OUT_NHWC_F16, OUT_ROWS_F32, check, lib)
+from ._lib import (ACT_NONE, ACT_QUICK_GELU, AttentionArgs, ConvArgs, ConvPlanInfo, DdimArgs, GroupNormArgs,
+                   OUT_GEGLU_F16, OUT_NCHW_F32, OUT_NHWC_F16, OUT_ROWS_F32, check, lib)
 
 BK = 64          # K tile of the conv kernel (packed weight column padding)
 BN = 128         # packed weight row padding (the kernels clamp reads beyond it)
@@ -265,7 +265,7 @@ AUTOTUNE = _Autotune()
 
 def conv2d(pc: PackedConv, x, *, ksize=None, stride=1, pad=None, pad_end=0, upsample=False, gn=None, silu=False,
            seg2=None, bias=True, row_bias=None, residual=None, out_mode=OUT_NHWC_F16, out=None,
-           variant=None, split_k=None):
+           variant=None, split_k=None, act=ACT_NONE):
     """Run the implicit-GEMM conv.  ``seg2`` = (x2, gn2, silu2) adds a fused 1x1 K segment.
     ``pad_end`` adds zero rows/cols after the source (asymmetric (0,1,0,1) padding).
     ``row_bias`` = (fp32 tensor [B, ld], column offset) — the per-(batch, channel) add.
@@ -286,6 +286,7 @@ def conv2d(pc: PackedConv, x, *, ksize=None, stride=1, pad=None, pad_end=0, upsa
         _fill_src(a.seg[1], x2, 1, 1, 0, False, gn2, silu2)
         a.nseg = 2
     a.batch, a.ho, a.wo, a.cout = B, Ho, Wo, pc.N
+    a.act = act
     a.weight = pc.weight.data_ptr()
     a.k_total = pc.k_total
     a.bias = pc.bias.data_ptr() if (bias and pc.bias is not None) else None
@@ -336,15 +337,17 @@ def conv2d(pc: PackedConv, x, *, ksize=None, stride=1, pad=None, pad_end=0, upsa
     return out
 
 
-def linear(pc: PackedConv, x2d, *, silu=False, residual=None, out_mode=OUT_NHWC_F16, out=None, bias=True):
-    """Token GEMM: x2d [M, K] fp16 → [M, N]; a 1x1 conv over an M x 1 image."""
+def linear(pc: PackedConv, x2d, *, silu=False, residual=None, out_mode=OUT_NHWC_F16, out=None, bias=True,
+           act=ACT_NONE):
+    """Token GEMM: x2d [M, K] fp16 → [M, N]; a 1x1 conv over an M x 1 image.  ``silu`` applies to
+    the input (prologue), ``act`` to the output (epilogue, before the residual)."""
     M = x2d.shape[0]
     x4 = x2d.view(1, M, 1, x2d.shape[-1]) if x2d.stride(-1) == 1 and x2d.is_contiguous() else None
     if x4 is None:
         x4 = x2d.as_strided((1, M, 1, x2d.shape[1]), (0, x2d.stride(0), x2d.stride(0), 1))
     res4 = residual.view(1, M, 1, residual.shape[-1]) if residual is not None else None
     y = conv2d(pc, x4, ksize=1, pad=0, silu=silu, residual=res4, out_mode=out_mode, bias=bias,
-               out=None if out is None else out.view(1, M, 1, out.shape[-1]))
+               out=None if out is None else out.view(1, M, 1, out.shape[-1]), act=act)
     return y.view(M, y.shape[-1])
 
 
@@ -427,8 +430,9 @@ def layer_norm(x2d, gamma, beta, eps=1e-5, out=None):
 
 # --------------------------------------------------------------------------- attention
 
-def attention(q, k, v, *, batch, heads, nq, nk, head_dim, scale, out=None):
-    """q/k/v: 2-D fp16 views [batch*n, ld] (head h at columns h*head_dim...)."""
+def attention(q, k, v, *, batch, heads, nq, nk, head_dim, scale, out=None, causal=False):
+    """q/k/v: 2-D fp16 views [batch*n, ld] (head h at columns h*head_dim...); ``causal`` masks
+    key j > query i."""
     for t, n in ((q, "q"), (k, "k"), (v, "v")):
         _need_cuda(t, "attention " + n)
     if out is None:
@@ -437,6 +441,7 @@ def attention(q, k, v, *, batch, heads, nq, nk, head_dim, scale, out=None):
     a.q, a.k, a.v, a.o = q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr()
     a.q_ld, a.k_ld, a.v_ld, a.o_ld = q.stride(0), k.stride(0), v.stride(0), out.stride(0)
     a.batch, a.heads, a.nq, a.nk, a.head_dim, a.scale = batch, heads, nq, nk, head_dim, scale
+    a.causal = 1 if causal else 0
     if PROFILER.active:
         PROFILER.begin("attention", (batch, heads, nq, nk, head_dim))
     check(lib().sdk_attention(C.byref(a), _stream()), "attention")
@@ -446,6 +451,20 @@ def attention(q, k, v, *, batch, heads, nq, nk, head_dim, scale, out=None):
 
 
 # --------------------------------------------------------------------------- sampler glue
+
+def token_embedding(ids: torch.Tensor, tok: torch.Tensor, pos: torch.Tensor):
+    """CLIP token + position embedding: ids int64 [B, T] → fp16 [B, T, D] (fp32 tables)."""
+    _need_cuda(ids, "token_embedding", torch.int64)
+    _need_cuda(tok, "token_embedding table", torch.float32)
+    _need_cuda(pos, "token_embedding positions", torch.float32)
+    B, T = ids.shape
+    if T > pos.shape[0]:
+        raise ValueError(f"sd_amd.token_embedding: {T} tokens > {pos.shape[0]} positions")
+    out = torch.empty(B, T, tok.shape[1], dtype=torch.float16, device=ids.device)
+    check(lib().sdk_token_embedding(_ptr(ids.contiguous()), _ptr(tok), _ptr(pos), _ptr(out), B, T, tok.shape[1],
+                                    _stream()), "token_embedding")
+    return out
+
 
 def timestep_embedding(t: torch.Tensor, freqs: torch.Tensor, dim: int):
     _need_cuda(t, "timestep_embedding", torch.int64)

@@ -132,6 +132,25 @@ def test_linear_residual_geglu_rows_f32(ops, conv_variant):
     assert y32.dtype == torch.float32 and rel_l2(y32, ref32) < 2e-3
 
 
+@pytest.mark.parametrize("M,K,N,split", [(154, 768, 3072, None), (154, 3072, 768, None), (1024, 1280, 1280, 4)])
+def test_linear_quick_gelu_act(ops, conv_variant, M, K, N, split):
+    """Epilogue activation (CLIP fc1 quick_gelu) after bias, before the residual — every tile
+    config, the split-K reduce and the fp32 row output."""
+    x = _rand(M, K, seed=41)
+    w = torch.randn(N, K) / math.sqrt(K)
+    b = torch.randn(N) * 0.1
+    r = _rand(M, N, seed=42)
+    pc = ops.PackedConv([(w, K)], b, device=DEV)
+    h = x.float() @ w.half().float().T + b
+    qg = h * torch.sigmoid(1.702 * h)
+    x4 = x.to(DEV).view(1, M, 1, K)
+    y = ops.conv2d(pc, x4, ksize=1, pad=0, act=ops.ACT_QUICK_GELU, residual=r.to(DEV).view(1, M, 1, N),
+                   split_k=split).view(M, N)
+    assert rel_l2(y, qg.half().float() + r.float()) < 3e-3
+    y32 = ops.linear(pc, x.to(DEV), act=ops.ACT_QUICK_GELU, out_mode=ops.OUT_ROWS_F32)
+    assert rel_l2(y32, qg) < 2e-3
+
+
 def test_conv_nchw_f32_out(ops, conv_variant):
     B, H, W, Cin, Cout = 2, 16, 16, 64, 4
     x = _rand(B, H, W, Cin, seed=6)
@@ -201,6 +220,23 @@ def test_attention_strided_packed(ops, B, H, n, nk, d, packed):
     o = ops.attention(q, k, v, batch=B, heads=H, nq=n, nk=nk, head_dim=d, scale=d ** -0.5)
     ref = attention_core(q.cpu().float().contiguous().view(B, n, H, d), k.cpu().float().contiguous().view(B, nk, H, d),
                          v.cpu().float().contiguous().view(B, nk, H, d), d ** -0.5).reshape(B * n, C)
+    assert rel_l2(o, ref) < 3e-3
+
+
+@pytest.mark.parametrize("B,H,n,d", [(2, 12, 77, 64), (1, 2, 77, 64), (1, 4, 300, 64), (2, 8, 129, 40),
+                                      (1, 2, 520, 80)])
+def test_attention_causal(ops, B, H, n, d):
+    """Causal self-attention (CLIP text tower): key j masked for query i when j > i; diagonal
+    tiles masked per element, tiles past a workgroup's last query skipped."""
+    q = _rand(B, n, H, d, seed=51)
+    k = _rand(B, n, H, d, seed=52)
+    v = _rand(B, n, H, d, seed=53)
+    s = d ** -0.5
+    o = ops.attention(q.view(B * n, H * d).to(DEV), k.view(B * n, H * d).to(DEV), v.view(B * n, H * d).to(DEV),
+                      batch=B, heads=H, nq=n, nk=n, head_dim=d, scale=s, causal=True)
+    qf, kf, vf = (t.float().transpose(1, 2) for t in (q, k, v))
+    att = (qf @ kf.transpose(-1, -2)) * s + torch.full((n, n), float("-inf")).triu(1)
+    ref = (att.softmax(-1) @ vf).transpose(1, 2).reshape(B * n, H * d)
     assert rel_l2(o, ref) < 3e-3
 
 

@@ -232,3 +232,38 @@ def test_full_vae_encode_vs_oracle(sdk):
     print(f"VAE encode rel-L2 {err:.3e}")
     assert post.parameters.shape == (1, 8, 64, 64)
     assert err < 2e-2
+
+
+# ---------------------------------------------------------------- CLIP text encoder
+def test_tiny_clip_vs_transformers(sdk):
+    """FrozenCLIPEmbedder's text tower on the HIP path vs transformers' CLIPTextModel (golden)."""
+    from sd_amd.clip_encoder.modules import FrozenCLIPEmbedder
+    z = load("clip_tiny")
+    cfg = json.loads(bytes(z["cfg"]).decode())
+    m = FrozenCLIPEmbedder(device=DEV, config=cfg)
+    m.transformer.load_state_dict(weights_of(z))
+    y = m.encode_tokens(torch.from_numpy(z["ids"]))
+    assert y.shape == z["y"].shape and y.dtype == torch.float16
+    assert rel_l2(y, torch.from_numpy(z["y"])) < 1e-2
+
+
+def test_full_clip_vit_l14_vs_oracle(sdk):
+    """ViT-L/14 text tower (123M params, 12 layers) at B=2 x 77 tokens vs the fp32 CPU oracle."""
+    from oracle.clip_ref import clip_text_forward
+    from sd_amd.clip_encoder.modules import FrozenCLIPEmbedder
+    with torch.device("meta"):
+        m = FrozenCLIPEmbedder(device=DEV)
+    ks = [(k, tuple(v.shape)) for k, v in m.transformer.state_dict().items()]
+    sd = {k: torch.from_numpy(v) for k, v in synth_weights(ks, 91).items()}
+    m = FrozenCLIPEmbedder(device=DEV)
+    m.transformer.load_state_dict(sd)
+    g = torch.Generator().manual_seed(92)
+    ids = torch.randint(0, 49406, (2, 77), generator=g)
+    ids[:, 0] = 49406
+    ids[0, 12:] = 49407
+    y = m(ids)
+    ref = clip_text_forward(sd, ids, 12)
+    err = rel_l2(y, ref)
+    print(f"CLIP ViT-L/14 rel-L2 {err:.3e}")
+    assert y.shape == (2, 77, 768)
+    assert err < 2e-2

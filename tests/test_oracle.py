@@ -138,3 +138,16 @@ def test_ddim_decode_from_t_start_bitexact():
                          ).astype(np.float32)
     out = sch.ddim_decode(z["enc_t30"], stub, tab, 5)
     assert np.array_equal(out, z["dec_t5"]), np.max(np.abs(out - z["dec_t5"]))
+
+
+# ---------------------------------------------------------------- CLIP text encoder
+def test_clip_text_vs_transformers():
+    import json
+    from oracle.clip_ref import clip_text_forward
+    z = load("clip_tiny")
+    cfg = json.loads(bytes(z["cfg"]).decode())
+    sd = {("text_model." + k if not k.startswith("text_model.") else k): v for k, v in weights_of(z).items()}
+    y = clip_text_forward(sd, torch.from_numpy(z["ids"]), cfg["num_attention_heads"], cfg["layer_norm_eps"])
+    ref = z["y"]
+    assert y.shape == ref.shape
+    assert np.max(np.abs(y.numpy() - ref)) <= 1e-4 * max(1.0, np.abs(ref).max())
