@@ -223,6 +223,19 @@ int sdk_stochastic_encode(const float* x0, const float* noise, float* out, int64
 int sdk_token_embedding(const int64_t* ids, const float* tok, const float* pos, void* out, int32_t batch,
                         int32_t seq, int32_t dim, sdk_stream_t stream);
 
+/* Tiled first-stage decode (ldm/diffusion/ddpm.py:1097-1139 with
+ * get_fold_unfold / get_weighting / delta_border :829-997, CompVis semantics — see DESIGN.md Q14):
+ * extract: latent NCHW fp32 [batch][channels][h][w] -> patches [L][batch][channels][kh][kw],
+ *   L = Ly*Lx, Ly = (h-kh)/sy + 1, patch l = ly*Lx + lx (torch.nn.Unfold order);
+ * fold: decoded patches [L][batch][channels][ph][pw] -> out [batch][channels][h][w] =
+ *   sum_l w*patch / sum_l w with w = pix_w[i][j] * l_w[l] (l_w may be NULL), the per-pixel
+ *   normalised overlap-add that Fold(o*weighting) / Fold(weighting) computes. */
+int sdk_extract_patches(const float* z, float* out, int32_t batch, int32_t channels, int32_t h, int32_t w,
+                        int32_t kh, int32_t kw, int32_t sy, int32_t sx, sdk_stream_t stream);
+int sdk_fold_patches(const float* patches, const float* pix_w, const float* l_w, float* out, int32_t batch,
+                     int32_t channels, int32_t h, int32_t w, int32_t ph, int32_t pw, int32_t sy, int32_t sx,
+                     int32_t ly, int32_t lx, sdk_stream_t stream);
+
 /* ---------------------------------------------------------------- introspection */
 const char* sdk_last_error(void);
 int sdk_version(void);

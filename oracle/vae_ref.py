@@ -173,3 +173,38 @@ def posterior_sample(moments: torch.Tensor, noise=None, scale_factor: float = 1.
         return scale_factor * mean
     std = torch.exp(0.5 * torch.clamp(logvar, -30.0, 20.0))
     return scale_factor * (mean + std * noise)
+
+
+def delta_border(h: int, w: int) -> torch.Tensor:
+    """CompVis ``delta_border`` (``ldm/diffusion/ddpm.py:838-859`` with the per-pixel min over the last
+    dim; the reference's dim=1 fails in torch.cat for w > 1 — DESIGN.md Q14)."""
+    y = torch.arange(0, h).view(h, 1, 1).repeat(1, w, 1)
+    x = torch.arange(0, w).view(1, w, 1).repeat(h, 1, 1)
+    arr = torch.cat([y, x], dim=-1) / torch.tensor([h - 1, w - 1]).view(1, 1, 2)
+    lu = torch.min(arr, dim=-1, keepdim=True)[0]
+    rd = torch.min(1 - arr, dim=-1, keepdim=True)[0]
+    return torch.min(torch.cat([lu, rd], dim=-1), dim=-1)[0]
+
+
+@torch.no_grad()
+def decode_first_stage_tiled(sd: dict, ddconfig: dict, z: torch.Tensor, scale_factor: float, sp: dict):
+    """Patch decode (``ldm/diffusion/ddpm.py:1097-1139``; ``get_fold_unfold`` uf>1 branch ``:894-960``;
+    ``get_weighting`` ``:862-891``): Unfold latent patches, decode each, weight, Fold, normalise."""
+    ks, stride, uf = tuple(sp["ks"]), tuple(sp["stride"]), int(sp["vqf"])
+    z = 1.0 / scale_factor * z.float()
+    bs, nc, h, w = z.shape
+    Ly, Lx = (h - ks[0]) // stride[0] + 1, (w - ks[1]) // stride[1] + 1
+    unfold = torch.nn.Unfold(kernel_size=ks, dilation=1, padding=0, stride=stride)
+    fold = torch.nn.Fold(output_size=(h * uf, w * uf), kernel_size=(ks[0] * uf, ks[1] * uf), dilation=1, padding=0,
+                         stride=(stride[0] * uf, stride[1] * uf))
+    wt = torch.clip(delta_border(ks[0] * uf, ks[1] * uf), sp["clip_min_weight"], sp["clip_max_weight"])
+    wt = wt.view(1, ks[0] * uf * ks[1] * uf, 1).repeat(1, 1, Ly * Lx)
+    if sp.get("tie_braker", False):
+        lw = torch.clip(delta_border(Ly, Lx), sp["clip_min_tie_weight"], sp["clip_max_tie_weight"])
+        wt = wt * lw.view(1, 1, Ly * Lx)
+    normalization = fold(wt).view(1, 1, h * uf, w * uf)
+    wt = wt.view(1, 1, ks[0] * uf, ks[1] * uf, Ly * Lx)
+    zp = unfold(z).view(bs, -1, ks[0], ks[1], Ly * Lx)
+    o = torch.stack([autoencoder_decode(sd, ddconfig, zp[:, :, :, :, i]) for i in range(Ly * Lx)], dim=-1)
+    o = (o * wt).view(bs, -1, Ly * Lx)
+    return fold(o) / normalization

@@ -10,9 +10,11 @@ logging, ``cond_stage_model`` — the conditioning tensor is passed in directly.
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 from torch import nn
 
+from .. import ops
 from ..DDIM.diffusion_modules import register_schedule
 from .utils import instantiate_from_config
 
@@ -94,4 +96,62 @@ class LatentDiffusion(nn.Module):
 
     @torch.no_grad()
     def decode_first_stage(self, z, predict_cids=False, force_not_quantize=False):
+        """``ldm/diffusion/ddpm.py:1083-1156``: z / scale_factor → first-stage decode; with
+        ``split_input_params['patch_distributed_vq']`` the tiled (patch) decode."""
+        sp = getattr(self, "split_input_params", None)
+        if sp and sp.get("patch_distributed_vq"):
+            return self._decode_tiled(z, sp)
         return self.first_stage_model.decode(z, pre_scale=1.0 / self.scale_factor)
+
+    # ------------------------------------------------------------------ tiled decode (SURVEY §8(f) rank 4)
+    @staticmethod
+    def delta_border(h, w):
+        """Normalised distance of each pixel to the nearest border (0 at the border, 0.5 at the
+        centre): min(y/(h-1), x/(w-1), 1-y/(h-1), 1-x/(w-1)) in fp32 — the CompVis semantics of
+        ``ldm/diffusion/ddpm.py:838-859``; the reference takes its first min over dim=1 and then
+        fails in torch.cat for any w > 1."""
+        f32 = np.float32
+        y = np.arange(h, dtype=np.int64)[:, None].astype(f32) / f32(h - 1)
+        x = np.arange(w, dtype=np.int64)[None, :].astype(f32) / f32(w - 1)
+        y, x = np.broadcast_to(y, (h, w)), np.broadcast_to(x, (h, w))
+        lu = np.minimum(y, x)
+        rd = np.minimum(f32(1.0) - y, f32(1.0) - x)
+        return np.minimum(lu, rd).astype(f32)
+
+    def get_weighting(self, h, w, Ly, Lx, sp):
+        """Pixel weights [h, w] and (tie-breaker) patch weights [Ly*Lx] or None
+        (``ldm/diffusion/ddpm.py:862-891``; weighting = pixel ⊗ patch, kept separable)."""
+        pix = np.clip(self.delta_border(h, w), sp["clip_min_weight"], sp["clip_max_weight"]).astype(np.float32)
+        lw = None
+        if sp.get("tie_braker", False):
+            lo = sp.get("clip_min_tie_weight", sp.get("clip_min_the_weight"))
+            hi = sp.get("clip_max_tie_weight", sp.get("clip_max_the_weight"))
+            lw = np.clip(self.delta_border(Ly, Lx), lo, hi).astype(np.float32).reshape(-1)
+        return pix, lw
+
+    def _decode_tiled(self, z, sp):
+        """Patch decode (``ldm/diffusion/ddpm.py:1097-1139`` + ``get_fold_unfold`` uf branch
+        ``:894-960``): latent patches of ``ks`` every ``stride`` are decoded as one batch
+        (chunks of ``sp.get('max_batch', 16)`` patches·images), weighted and overlap-added at
+        uf = vqf on the device (``sdk_extract_patches`` / ``sdk_fold_patches``)."""
+        ks, stride, uf = tuple(sp["ks"]), tuple(sp["stride"]), int(sp["vqf"])
+        B, Cz, h, w = z.shape
+        ks = (min(ks[0], h), min(ks[1], w))
+        stride = (min(stride[0], h), min(stride[1], w))
+        Ly, Lx = (h - ks[0]) // stride[0] + 1, (w - ks[1]) // stride[1] + 1
+        key = (ks, stride, uf, Ly, Lx, z.device)
+        cache = getattr(self, "_tile_w", None)
+        if cache is None or cache[0] != key:
+            pix, lw = self.get_weighting(ks[0] * uf, ks[1] * uf, Ly, Lx, sp)
+            cache = (key, torch.from_numpy(pix).to(z.device),
+                     torch.from_numpy(lw).to(z.device) if lw is not None else None)
+            self._tile_w = cache
+        _, pix_w, l_w = cache
+        patches = ops.extract_patches(z.float(), ks[0], ks[1], stride[0], stride[1])   # [L, B, C, kh, kw]
+        flat = patches.view(Ly * Lx * B, Cz, ks[0], ks[1])
+        chunk = int(sp.get("max_batch", 16))
+        dec = [self.first_stage_model.decode(flat[i:i + chunk], pre_scale=1.0 / self.scale_factor)
+               for i in range(0, flat.shape[0], chunk)]
+        dec = torch.cat(dec, 0) if len(dec) > 1 else dec[0]
+        dec = dec.view(Ly * Lx, B, dec.shape[1], dec.shape[2], dec.shape[3])
+        return ops.fold_patches(dec, pix_w, l_w, h * uf, w * uf, stride[0] * uf, stride[1] * uf, Ly, Lx)

@@ -60,7 +60,8 @@ ACT_NONE, ACT_QUICK_GELU = 0, 1
 
 EXPORTS = ["sdk_conv2d_plan", "sdk_conv2d", "sdk_group_norm_workspace", "sdk_group_norm_affine", "sdk_group_norm_apply", "sdk_layer_norm",
            "sdk_attention", "sdk_ddim_step", "sdk_ddpm_step", "sdk_timestep_embedding", "sdk_nchw_to_nhwc",
-           "sdk_diag_gaussian_sample", "sdk_stochastic_encode", "sdk_token_embedding", "sdk_last_error", "sdk_version", "sdk_kernel_name"]
+           "sdk_diag_gaussian_sample", "sdk_stochastic_encode", "sdk_token_embedding", "sdk_extract_patches",
+           "sdk_fold_patches", "sdk_last_error", "sdk_version", "sdk_kernel_name"]
 
 _lib = None
 
@@ -87,6 +88,8 @@ def lib():
     L.sdk_diag_gaussian_sample.argtypes = [vp, vp, vp, i32, i32, i32, f32, vp]
     L.sdk_stochastic_encode.argtypes = [vp, vp, vp, i64, f32, f32, vp]
     L.sdk_token_embedding.argtypes = [vp, vp, vp, vp, i32, i32, i32, vp]
+    L.sdk_extract_patches.argtypes = [vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp]
+    L.sdk_fold_patches.argtypes = [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp]
     L.sdk_last_error.restype = C.c_char_p
     L.sdk_kernel_name.restype = C.c_char_p
     L.sdk_kernel_name.argtypes = [i32]

@@ -158,10 +158,81 @@ __global__ void __launch_bounds__(128) token_embedding_kernel(const int64_t* ids
   }
 }
 
+// patch p = ((ly*Lx + lx)*B + b): out[p][c][i][j] = z[b][c][ly*sy + i][lx*sx + j] (torch.nn.Unfold order)
+__global__ void __launch_bounds__(256) extract_patches_kernel(const float* z, float* out, int B, int C, int H, int W,
+                                                              int kh, int kw, int sy, int sx, int Lx, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += stride) {
+    const int j = (int)(e % kw);
+    int64_t r = e / kw;
+    const int i = (int)(r % kh); r /= kh;
+    const int c = (int)(r % C); r /= C;
+    const int b = (int)(r % B);
+    const int l = (int)(r / B);
+    const int ly = l / Lx, lx = l - ly * Lx;
+    out[e] = z[(((int64_t)b * C + c) * H + ly * sy + i) * W + lx * sx + j];
+  }
+}
+
+// overlap-add of weighted decoded patches, normalised per pixel:
+// out = sum_l w(l, y, x) * patch_l / sum_l w(l, y, x), w = pix_w[i][j] * (l_w ? l_w[l] : 1)
+// (torch.nn.Fold of o*weighting divided by Fold(weighting)); one thread per output element
+// gathers the <= ceil(ph/sy) x ceil(pw/sx) covering patches — no atomics, deterministic
+__global__ void __launch_bounds__(256) fold_patches_kernel(const float* patches, const float* pix_w, const float* l_w,
+                                                           float* out, int B, int C, int H, int W, int ph, int pw,
+                                                           int sy, int sx, int Ly, int Lx, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += stride) {
+    const int x = (int)(e % W);
+    int64_t r = e / W;
+    const int y = (int)(r % H); r /= H;
+    const int c = (int)(r % C);
+    const int b = (int)(r / C);
+    const int ly0 = y >= ph ? (y - ph) / sy + 1 : 0, ly1 = min(Ly - 1, y / sy);
+    const int lx0 = x >= pw ? (x - pw) / sx + 1 : 0, lx1 = min(Lx - 1, x / sx);
+    float num = 0.f, den = 0.f;
+    for (int ly = ly0; ly <= ly1; ++ly)
+      for (int lx = lx0; lx <= lx1; ++lx) {
+        const int l = ly * Lx + lx, i = y - ly * sy, j = x - lx * sx;
+        float w = pix_w[i * pw + j];
+        if (l_w) w = w * l_w[l];
+        const float v = patches[((((int64_t)l * B + b) * C + c) * ph + i) * pw + j];
+        num = num + v * w;
+        den = den + w;
+      }
+    out[e] = num / den;   // 0/0 = NaN where no patch covers the pixel, as Fold / normalization
+  }
+}
+
 }  // namespace
 }  // namespace sdk
 
 using namespace sdk;
+
+extern "C" int sdk_extract_patches(const float* z, float* out, int32_t batch, int32_t channels, int32_t h, int32_t w,
+                                   int32_t kh, int32_t kw, int32_t sy, int32_t sx, sdk_stream_t stream) {
+  if (!z || !out || batch <= 0 || channels <= 0 || kh <= 0 || kw <= 0 || sy <= 0 || sx <= 0 || kh > h || kw > w)
+    return fail(SDK_EINVAL, "extract_patches: bad geometry");
+  const int Ly = (h - kh) / sy + 1, Lx = (w - kw) / sx + 1;
+  const int64_t n = (int64_t)Ly * Lx * batch * channels * kh * kw;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(extract_patches_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, z, out, batch, channels,
+                     h, w, kh, kw, sy, sx, Lx, n);
+  return check_launch("extract_patches");
+}
+
+extern "C" int sdk_fold_patches(const float* patches, const float* pix_w, const float* l_w, float* out, int32_t batch,
+                                int32_t channels, int32_t h, int32_t w, int32_t ph, int32_t pw, int32_t sy, int32_t sx,
+                                int32_t ly, int32_t lx, sdk_stream_t stream) {
+  if (!patches || !pix_w || !out || batch <= 0 || channels <= 0 || ph <= 0 || pw <= 0 || sy <= 0 || sx <= 0 ||
+      ly <= 0 || lx <= 0 || (ly - 1) * sy + ph > h || (lx - 1) * sx + pw > w)
+    return fail(SDK_EINVAL, "fold_patches: bad geometry");
+  const int64_t n = (int64_t)batch * channels * h * w;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(fold_patches_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, patches, pix_w, l_w, out,
+                     batch, channels, h, w, ph, pw, sy, sx, ly, lx, n);
+  return check_launch("fold_patches");
+}
 
 extern "C" int sdk_token_embedding(const int64_t* ids, const float* tok, const float* pos, void* out, int32_t batch,
                                    int32_t seq, int32_t dim, sdk_stream_t stream) {

@@ -466,6 +466,31 @@ def token_embedding(ids: torch.Tensor, tok: torch.Tensor, pos: torch.Tensor):
     return out
 
 
+def extract_patches(z: torch.Tensor, kh: int, kw: int, sy: int, sx: int):
+    """NCHW fp32 [B, C, H, W] → patches [Ly*Lx, B, C, kh, kw] (torch.nn.Unfold patch order)."""
+    _need_cuda(z, "extract_patches", torch.float32)
+    z = z.contiguous()
+    B, Cc, H, W = z.shape
+    Ly, Lx = (H - kh) // sy + 1, (W - kw) // sx + 1
+    out = torch.empty(Ly * Lx, B, Cc, kh, kw, dtype=torch.float32, device=z.device)
+    check(lib().sdk_extract_patches(_ptr(z), _ptr(out), B, Cc, H, W, kh, kw, sy, sx, _stream()), "extract_patches")
+    return out
+
+
+def fold_patches(patches: torch.Tensor, pix_w: torch.Tensor, l_w, H: int, W: int, sy: int, sx: int, Ly: int,
+                 Lx: int):
+    """[L, B, C, ph, pw] fp32 → normalised weighted overlap-add [B, C, H, W]."""
+    _need_cuda(patches, "fold_patches", torch.float32)
+    _need_cuda(pix_w, "fold_patches weights", torch.float32)
+    patches = patches.contiguous()
+    L, B, Cc, ph, pw = patches.shape
+    assert L == Ly * Lx
+    out = torch.empty(B, Cc, H, W, dtype=torch.float32, device=patches.device)
+    check(lib().sdk_fold_patches(_ptr(patches), _ptr(pix_w.contiguous()), _ptr(l_w), _ptr(out), B, Cc, H, W, ph, pw,
+                                 sy, sx, Ly, Lx, _stream()), "fold_patches")
+    return out
+
+
 def timestep_embedding(t: torch.Tensor, freqs: torch.Tensor, dim: int):
     _need_cuda(t, "timestep_embedding", torch.int64)
     out = torch.empty(t.shape[0], dim, dtype=torch.float16, device=t.device)

@@ -343,6 +343,60 @@ def gen_img2img(fake):
     np.savez_compressed(os.path.join(OUT, "img2img.npz"), **out)
 
 
+def gen_tiled_decode():
+    """SURVEY §8(f) rank 4 — patch (split_input_params) decode: the reference's own
+    get_fold_unfold / get_weighting / meshgrid (Diffusion/ddpm.py, same code as
+    ldm/diffusion/ddpm.py:829-997) on a stand-in object, with delta_border's first min taken
+    over the last dim (test-only shim: as written, dim=1 fails in torch.cat for w > 1 — DESIGN.md
+    Q14), the tiny reference VAE decoding each patch, composed as ldm/diffusion/ddpm.py:1097-1139."""
+    with quiet():
+        import Unet.unet as uu
+        import Encoder_Decoder.encoder as ee
+        silu = lambda x: x * torch.sigmoid(x)
+        uu.nonlinearity = silu
+        ee.nonlinearity = silu
+        from VAE.autoencoder import AutoEncoderKL
+        from Diffusion.ddpm import LatentDiffusion as RefLD
+        vae = AutoEncoderKL(ddconfig=dict(TINY_VAE), embed_dim=4, lossconfig={"target": "torch.nn.Identity"})
+    reinit_(vae, 15)
+    vae.eval()
+    sp = {"patch_distributed_vq": True, "ks": (8, 8), "stride": (4, 4), "vqf": 2, "clip_min_weight": 0.01,
+          "clip_max_weight": 0.5, "tie_braker": True, "clip_min_tie_weight": 0.01, "clip_max_tie_weight": 0.5}
+
+    def delta_border(self, h, w):
+        lower_right_corner = torch.tensor([h - 1, w - 1]).view(1, 1, 2)
+        arr = self.meshgrid(h, w) / lower_right_corner
+        dist_left_up = torch.min(arr, dim=-1, keepdim=True)[0]
+        dist_right_down = torch.min(1 - arr, dim=-1, keepdim=True)[0]
+        return torch.min(torch.cat([dist_left_up, dist_right_down], dim=-1), dim=-1)[0]
+
+    class Stand:
+        split_input_params = sp
+        meshgrid = RefLD.meshgrid
+        get_weighting = RefLD.get_weighting
+        get_fold_unfold = RefLD.get_fold_unfold
+
+    Stand.delta_border = delta_border
+    st = Stand()
+    g = torch.Generator().manual_seed(16)
+    zl = torch.randn(2, 4, 16, 16, generator=g)
+    scale_factor = 0.18215
+    z = 1.0 / scale_factor * zl
+    ks, stride, uf = sp["ks"], sp["stride"], sp["vqf"]
+    with quiet(), torch.no_grad():
+        fold, unfold, normalization, weighting = st.get_fold_unfold(z, ks, stride, uf=uf)
+        zp = unfold(z)
+        zp = zp.view((zp.shape[0], -1, ks[0], ks[1], zp.shape[-1]))
+        o = torch.stack([vae.decode(zp[:, :, :, :, i]) for i in range(zp.shape[-1])], axis=-1)
+        o = o * weighting
+        o = o.view((o.shape[0], -1, o.shape[-1]))
+        dec = fold(o) / normalization
+    np.savez_compressed(os.path.join(OUT, "vae_tiled.npz"), **sd_keys(vae), seed=np.int64(15), z=zl.numpy(),
+                        dec=dec.numpy(), scale_factor=np.float64(scale_factor),
+                        sp=np.frombuffer(json.dumps(sp).encode(), dtype=np.uint8),
+                        cfg=np.frombuffer(json.dumps(TINY_VAE).encode(), dtype=np.uint8))
+
+
 def gen_ddpm():
     """C1 pipeline: DDPMPipeline tables + a 10-step sampling run with a recorded-ε
     stub model and recorded noise (DDPM/ddpm.py:17-89)."""
@@ -385,6 +439,7 @@ def main():
     gen_unet("unet_tiny_headch", TINY_UNET_HC, 9, with_ctx=True)
     gen_vae()
     gen_img2img(fake)
+    gen_tiled_decode()
     gen_ddpm()
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):

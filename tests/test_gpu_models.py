@@ -267,3 +267,54 @@ def test_full_clip_vit_l14_vs_oracle(sdk):
     print(f"CLIP ViT-L/14 rel-L2 {err:.3e}")
     assert y.shape == (2, 77, 768)
     assert err < 2e-2
+
+
+# ---------------------------------------------------------------- tiled decode
+def test_tiled_decode_vs_reference(sdk):
+    """LatentDiffusion.decode_first_stage with split_input_params (patch decode, pixel + tie-breaker
+    weights, normalised overlap-add) vs the reference's fold/unfold/weighting (golden)."""
+    from sd_amd.Diffusion.ddpm import LatentDiffusion
+    from sd_amd.VAE.autoencoder import AutoEncoderKL
+    z = load("vae_tiled")
+    sp = json.loads(bytes(z["sp"]).decode())
+    vae = AutoEncoderKL(ddconfig=cfg_of(z), embed_dim=4)
+    vae.load_state_dict(weights_of(z))
+
+    class LD:                      # the decode_first_stage surface of LatentDiffusion
+        scale_factor = float(z["scale_factor"])
+        first_stage_model = vae
+        split_input_params = sp
+        decode_first_stage = LatentDiffusion.decode_first_stage
+        _decode_tiled = LatentDiffusion._decode_tiled
+        get_weighting = LatentDiffusion.get_weighting
+        delta_border = staticmethod(LatentDiffusion.delta_border)
+
+    dec = LD().decode_first_stage(torch.from_numpy(z["z"]).to(DEV))
+    assert dec.shape == z["dec"].shape
+    assert rel_l2(dec, torch.from_numpy(z["dec"])) < 1e-2
+
+
+@pytest.mark.parametrize("H,W,ph,pw,sy,sx,tie", [(64, 48, 32, 16, 16, 8, True), (40, 40, 24, 24, 8, 8, False)])
+def test_fold_patches_vs_torch(sdk, H, W, ph, pw, sy, sx, tie):
+    """Normalised weighted overlap-add vs torch.nn.Fold(o*w) / Fold(w); patch extraction vs Unfold."""
+    from sd_amd import ops
+    B, Cc = 2, 3
+    Ly, Lx = (H - ph) // sy + 1, (W - pw) // sx + 1
+    g = torch.Generator().manual_seed(H)
+    pat = torch.randn(Ly * Lx, B, Cc, ph, pw, generator=g)
+    pix = torch.rand(ph, pw, generator=g) + 0.01
+    lw = torch.rand(Ly * Lx, generator=g) + 0.01 if tie else None
+    out = ops.fold_patches(pat.to(DEV), pix.to(DEV), lw.to(DEV) if tie else None, H, W, sy, sx, Ly, Lx)
+    wt = pix.view(1, ph * pw, 1).repeat(1, 1, Ly * Lx)
+    if tie:
+        wt = wt * lw.view(1, 1, -1)
+    fold = torch.nn.Fold(output_size=(H, W), kernel_size=(ph, pw), stride=(sy, sx))
+    o = (pat.permute(1, 2, 3, 4, 0) * wt.view(1, 1, ph, pw, -1)).reshape(B, -1, Ly * Lx)
+    ref = fold(o) / fold(wt).view(1, 1, H, W)
+    cov = ref.isfinite()
+    assert torch.equal(out.cpu().isfinite(), cov)
+    assert torch.allclose(out.cpu()[cov], ref[cov], rtol=1e-5, atol=1e-5)
+    zimg = torch.randn(B, Cc, H, W, generator=g)
+    got = ops.extract_patches(zimg.to(DEV), ph, pw, sy, sx).cpu()
+    unf = torch.nn.Unfold(kernel_size=(ph, pw), stride=(sy, sx))(zimg).view(B, Cc, ph, pw, -1).permute(4, 0, 1, 2, 3)
+    assert torch.equal(got, unf)

@@ -151,3 +151,15 @@ def test_clip_text_vs_transformers():
     ref = z["y"]
     assert y.shape == ref.shape
     assert np.max(np.abs(y.numpy() - ref)) <= 1e-4 * max(1.0, np.abs(ref).max())
+
+
+# ---------------------------------------------------------------- tiled decode
+def test_tiled_decode_vs_reference():
+    import json
+    z = load("vae_tiled")
+    cfg, sd = cfg_of(z), weights_of(z)
+    sp = json.loads(bytes(z["sp"]).decode())
+    dec = vae_ref.decode_first_stage_tiled(sd, cfg, torch.from_numpy(z["z"]), float(z["scale_factor"]), sp)
+    ref = z["dec"]
+    assert dec.shape == ref.shape
+    assert np.max(np.abs(dec.numpy() - ref)) <= 1e-4 * max(1.0, np.abs(ref).max())
