@@ -143,6 +143,12 @@ int sdk_group_norm_affine(const sdk_group_norm_args* a, sdk_stream_t stream);
  * openai_model/model.py:178-181,202-205,528-530; Unet/unet.py:116-125; encoder.py:205-206). */
 int sdk_group_norm_apply(const sdk_group_norm_args* a, int32_t silu, void* y, int32_t ld_y, sdk_stream_t stream);
 
+/* The same, written into a zero-bordered image y [batch][h+2*pad][w+2*pad][ld_y] (h*w == hw): the
+ * 3x3 conv that consumes it runs with pad 0, so its implicit-GEMM gather has every tap in range
+ * (no per-tap masks — the zero padding of nn.Conv2d(padding=1) is stored, not computed). */
+int sdk_group_norm_apply_padded(const sdk_group_norm_args* a, int32_t silu, void* y, int32_t ld_y, int32_t h,
+                                int32_t w, int32_t pad, sdk_stream_t stream);
+
 /* ---------------------------------------------------------------- LayerNorm
  * y = (x - mean) * rstd * gamma + beta over the last dim, fp16 in/out, fp32 math.
  * Replaces nn.LayerNorm norm1/2/3 (openai_model/attention.py:216-218,251-253).

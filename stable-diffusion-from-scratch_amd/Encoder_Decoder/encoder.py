@@ -101,8 +101,9 @@ class Encoder(nn.Module):
         h = self.mid.block_1._run(h)
         h = self.mid.attn_1._run(h)
         h = self.mid.block_2._run(h)
-        ha = ops.group_norm_apply(h, gn_stats(self.norm_out, h), silu=True)
-        return ops.conv2d(self._pc_out, ha, out_mode=ops.OUT_NCHW_F32)
+        gp, cp = ops.gn_conv_pad()
+        ha = ops.group_norm_apply(h, gn_stats(self.norm_out, h), silu=True, pad=gp)
+        return ops.conv2d(self._pc_out, ha, pad=cp, out_mode=ops.OUT_NCHW_F32)
 
     @torch.no_grad()
     def forward(self, x):
@@ -189,8 +190,9 @@ class Decoder(nn.Module):
             raise NotImplementedError("sd_amd: give_pre_end is not on the SD path")
         if self.tanh_out:
             raise NotImplementedError("sd_amd: tanh_out is not on the SD path")
-        ha = ops.group_norm_apply(h, gn_stats(self.norm_out, h), silu=True)
-        return ops.conv2d(self._pc_out, ha, out_mode=ops.OUT_NCHW_F32)
+        gp, cp = ops.gn_conv_pad()
+        ha = ops.group_norm_apply(h, gn_stats(self.norm_out, h), silu=True, pad=gp)
+        return ops.conv2d(self._pc_out, ha, pad=cp, out_mode=ops.OUT_NCHW_F32)
 
     @torch.no_grad()
     def forward(self, z):

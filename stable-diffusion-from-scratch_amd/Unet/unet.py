@@ -105,10 +105,12 @@ class ResnetBlock(nn.Module):
     def _run(self, x, temb=None):
         if temb is not None:
             raise NotImplementedError("sd_amd: the VAE ResnetBlock path has no timestep embedding")
-        h = ops.conv2d(self._pc1, ops.group_norm_apply(x, gn_stats(self.norm1, x), silu=True))
-        ha = ops.group_norm_apply(h, gn_stats(self.norm2, h), silu=True)
+        # zero-bordered GN+SiLU outputs: both 3x3 convs run with pad 0 (mask-free gather)
+        gp, cp = ops.gn_conv_pad()
+        h = ops.conv2d(self._pc1, ops.group_norm_apply(x, gn_stats(self.norm1, x), silu=True, pad=gp), pad=cp)
+        ha = ops.group_norm_apply(h, gn_stats(self.norm2, h), silu=True, pad=gp)
         if self._mode == "identity":
-            return ops.conv2d(self._pc2, ha, residual=x)
+            return ops.conv2d(self._pc2, ha, pad=cp, residual=x)
         if self._mode == "fused":
-            return ops.conv2d(self._pc2, ha, seg2=(x, None, False))
-        return ops.conv2d(self._pc2, ha, residual=ops.conv2d(self._pcs, x))
+            return ops.conv2d(self._pc2, ha, pad=cp, seg2=(x, None, False))
+        return ops.conv2d(self._pc2, ha, pad=cp, residual=ops.conv2d(self._pcs, x))

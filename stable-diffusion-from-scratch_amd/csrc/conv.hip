@@ -60,6 +60,8 @@ struct Params {
   int tiles_m, tiles_n;
   int variant;          // 0: register-staged 128x128 (A transforms); 2/3/4: LDS-DMA 256x256 / 256x128 / 128x128
   int act;              // epilogue activation after bias / embedding, before the residual (sdk_conv_act)
+  int nomask;           // segment 0 has every tap in range (pad 0, no pad_end / upsample, cin % 64 == 0):
+                        // the LDS-DMA A gather is a lane base + a scalar tap offset, no masks
 };
 
 // epilogue activation (CLIP's quick_gelu x*sigmoid(1.702x), transformers activations.py QuickGELUActivation)
@@ -896,6 +898,13 @@ __device__ __forceinline__ void dma_a_piece(const Params& p, const DmaSrc& d, ha
   const Seg& g0 = p.seg[0];
   const Seg& g1 = p.seg[1];
   const unsigned rch16 = (unsigned)rch * 16u;
+  if (seg == 0 && p.nomask) {
+    const bool second = cb >= g0.c_split;
+    const unsigned ld2 = (unsigned)(second ? g0.ld1 : g0.ld0) * 2u;
+    const unsigned toff = (unsigned)((ky * g0.w + kx) * (int)ld2 + (cb - (second ? g0.c_split : 0)) * 2);
+    ph_dma(second ? d.a1 : d.a0, dst, __umul24(pixb, ld2) + rch16 + toff, 0);
+    return;
+  }
   if (seg == 0) {
     const bool second = cb >= g0.c_split;
     const __amdgpu_buffer_rsrc_t r = second ? d.a1 : d.a0;
@@ -1287,9 +1296,16 @@ __global__ void __launch_bounds__(512) conv_ph_kernel(Params p) {
   do {                                                                                     \
     half_t* sl_ = lds + (SLOT) * PH_HALF + wave * 8 * BK;                                  \
     const int kt_ = kt0 + (T);                                                             \
-    if (DBG & 1) {                                                                         \
+    if (DBG & (1 | 256)) {                                                                 \
     } else if (kt_ >= kt1) {                                                               \
       _Pragma("unroll") for (int j = 0; j < 2; ++j) ph_dma(d.w, sl_ + j * 64 * BK, PH_OOB, 0); \
+    } else if (DBG & 512) {                                                                \
+      _Pragma("unroll") for (int j = 0; j < 2; ++j)                                        \
+        ph_dma(d.w, sl_ + j * 64 * BK, wv[(A_) * 2 + j], kt_ * BK * 2);                    \
+    } else if (DBG & 1024) {                                                               \
+      _Pragma("unroll") for (int j = 0; j < 2; ++j)                                        \
+        ph_dma(SEG == 0 ? d.a0 : d.s0, sl_ + j * 64 * BK,                                  \
+               __umul24(pixb[(A_) * 2 + j], (unsigned)p.seg[0].ld0 * 2u) + rch * 16u + (unsigned)(CB) * 2u, 0); \
     } else {                                                                               \
       _Pragma("unroll") for (int j = 0; j < 2; ++j)                                        \
         dma_a_piece(p, d, sl_ + j * 64 * BK, pixb[(A_) * 2 + j], msk[(A_) * 2 + j],         \
@@ -1300,7 +1316,7 @@ __global__ void __launch_bounds__(512) conv_ph_kernel(Params p) {
   do {                                                                                     \
     half_t* sl_ = lds + (SLOT) * PH_HALF + wave * 8 * BK;                                  \
     const int kt_ = kt0 + (T);                                                             \
-    if (DBG & 1) {                                                                         \
+    if (DBG & (1 | 128)) {                                                                 \
     } else if (kt_ >= kt1) {                                                               \
       _Pragma("unroll") for (int j = 0; j < 2; ++j) ph_dma(d.w, sl_ + j * 64 * BK, PH_OOB, 0); \
     } else {                                                                               \
@@ -1616,6 +1632,11 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
     kreal += (double)taps * g.cin;
   }
   if (koff != a->k_total) return fail(SDK_EINVAL, "conv2d: k_total does not match the packed segment layout");
+  {
+    const sdk_conv_src& g = a->seg[0];
+    p.nomask = g.pad == 0 && g.pad_end == 0 && !g.upsample && g.cin % BK == 0 &&
+               (g.c_split == g.cin || g.c_split % BK == 0) && g.gn_scale == nullptr && !g.silu;
+  }
   if (a->out_mode == SDK_OUT_NHWC_F16 || a->out_mode == SDK_OUT_GEGLU_F16) {
     if (a->cout % 8 || a->out_ld % 8 || (a->residual && a->res_ld % 8))
       return fail(SDK_EINVAL, "conv2d: fp16 NHWC output needs cout/out_ld/res_ld multiples of 8");
@@ -1687,13 +1708,13 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   // 16..19 deep-ring LDS-DMA configs; 20, 21 phased 256x256 on v_mfma_f32_16x16x32_f16;
   // 22..26 LDS-DMA configs 5, 7, 6, 19, 18 on v_mfma_f32_16x16x32_f16
   const int fbase = forced;
-  const bool fvalid = forced >= 0 && forced != 1 && forced <= 26;
+  const bool fvalid = forced >= 0 && forced != 1 && forced <= 30;
   const bool fgeglu = (fbase <= 4 || fbase >= 8) && fbase != 22 && fbase != 23 && fbase != 24;
   if (fvalid && (forced == 0 || !transform) && (fgeglu || a->out_mode != SDK_OUT_GEGLU_F16)) {
-    static const int fbm[27] = {128, 0, 256, 256, 128, 256, 256, 128, 256, 256, 256, 256, 256, 256, 256, 256,
-                                128, 256, 128, 128, 256, 256, 256, 128, 256, 128, 128};
-    static const int fbn[27] = {128, 0, 256, 128, 128, 320, 160, 320, 256, 256, 256, 256, 256, 256, 256, 256,
-                                128, 128, 128, 256, 256, 256, 320, 320, 160, 256, 128};
+    static const int fbm[31] = {128, 0, 256, 256, 128, 256, 256, 128, 256, 256, 256, 256, 256, 256, 256, 256,
+                                128, 256, 128, 128, 256, 256, 256, 128, 256, 128, 128, 256, 256, 256, 256};
+    static const int fbn[31] = {128, 0, 256, 128, 128, 320, 160, 320, 256, 256, 256, 256, 256, 256, 256, 256,
+                                128, 128, 128, 256, 256, 256, 320, 320, 160, 256, 128, 256, 256, 256, 256};
     var = forced;
     tbm = fbm[fbase];
     tbn = fbn[fbase];
@@ -1779,6 +1800,10 @@ extern "C" int sdk_conv2d(const sdk_conv_args* a, sdk_stream_t stream) {
     case 24: rc = launch_glds<Cfg256x160m>(p, s); break;
     case 25: rc = launch_glds<Cfg128x256r3m>(p, s); break;
     case 26: rc = launch_glds<Cfg128x128r3m>(p, s); break;
+    case 27: rc = launch_ph<PhCfg8, 128>(p, s); break;   // diagnostics: no W DMA issued
+    case 28: rc = launch_ph<PhCfg8, 256>(p, s); break;   // diagnostics: no A DMA issued
+    case 29: rc = launch_ph<PhCfg8, 512>(p, s); break;   // diagnostics: A DMAs read W rows (cheap addressing, L2)
+    case 30: rc = launch_ph<PhCfg8, 1024>(p, s); break;  // diagnostics: A DMAs read the centre tap (no masks/halo)
     default:
       hipLaunchKernelGGL(conv_igemm_kernel, grid, dim3(NT), 0, s, p);
       rc = check_launch("conv_igemm");

@@ -210,6 +210,41 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const half_t* s0, const h
   }
 }
 
+// The same transform written into a zero-bordered image [B][h+2p][w+2p][ldy]: the 3x3 conv that
+// consumes it runs with pad 0, every tap in range — no per-tap masks in its A gather.
+__global__ void __launch_bounds__(256) gn_apply_pad_kernel(const half_t* s0, const half_t* s1, int c_split, int ld0,
+                                                           int ld1, int h, int w, int pad, int channels,
+                                                           const float* scale, const float* shift, int silu,
+                                                           half_t* y, int ldy, int64_t nvec) {
+  const int c8 = channels / 8;
+  const int hp = h + 2 * pad, wp = w + 2 * pad;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nvec; e += stride) {
+    const int64_t ppix = e / c8;
+    const int c = (int)(e - ppix * c8) * 8;
+    const int b = (int)(ppix / ((int64_t)hp * wp));
+    const int r = (int)(ppix - (int64_t)b * hp * wp);
+    const int iy = r / wp - pad, ix = r % wp - pad;
+    h8 o = {};
+    if ((unsigned)iy < (unsigned)h && (unsigned)ix < (unsigned)w) {
+      const size_t pix = ((size_t)b * h + iy) * w + ix;
+      const h8 v = load_px(s0, s1, c_split, ld0, ld1, pix, c);
+      const f4* ps = reinterpret_cast<const f4*>(scale + (size_t)b * channels + c);
+      const f4* pt = reinterpret_cast<const f4*>(shift + (size_t)b * channels + c);
+      const f4 sa = ps[0], sb = ps[1], ta = pt[0], tb = pt[1];
+      const float sc[8] = {sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3]};
+      const float sh[8] = {ta[0], ta[1], ta[2], ta[3], tb[0], tb[1], tb[2], tb[3]};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float x = (float)v[j] * sc[j] + sh[j];
+        if (silu) x = x * __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+        o[j] = (half_t)x;
+      }
+    }
+    *reinterpret_cast<h8*>(y + (size_t)ppix * ldy + c) = o;
+  }
+}
+
 // LayerNorm: one wave per row, row cached in registers (cols <= 64*8*MAXV).
 constexpr int LN_MAXV = 4;
 __global__ void __launch_bounds__(256) layer_norm_kernel(const half_t* x, half_t* y, int rows, int cols, int ldx,
@@ -311,6 +346,24 @@ extern "C" int sdk_group_norm_apply(const sdk_group_norm_args* a, int32_t silu, 
                      (const half_t*)a->src1, a->c_split, a->ld0, a->ld1, a->hw, a->channels, a->scale, a->shift,
                      silu, (half_t*)y, ld_y, nvec);
   return check_launch("gn_apply");
+}
+
+extern "C" int sdk_group_norm_apply_padded(const sdk_group_norm_args* a, int32_t silu, void* y, int32_t ld_y,
+                                           int32_t h, int32_t w, int32_t pad, sdk_stream_t stream) {
+  if (!a || !a->src0 || !a->scale || !a->shift || !y) return fail(SDK_EINVAL, "group_norm_apply: null pointer");
+  if (a->channels % 8 || a->c_split % 8 || a->c_split <= 0 || a->c_split > a->channels || ld_y % 8 ||
+      ld_y < a->channels)
+    return fail(SDK_EINVAL, "group_norm_apply: channels/c_split/ld_y must be multiples of 8");
+  if (a->c_split < a->channels && !a->src1) return fail(SDK_EINVAL, "group_norm_apply: concat without src1");
+  if (h <= 0 || w <= 0 || (int64_t)h * w != a->hw || pad < 0 || pad > 4)
+    return fail(SDK_EINVAL, "group_norm_apply_padded: h*w must equal hw, pad in [0, 4]");
+  const int64_t nvec = (int64_t)a->batch * (h + 2 * pad) * (w + 2 * pad) * (a->channels / 8);
+  if (nvec <= 0) return SDK_OK;
+  const int blocks = (int)std::min<int64_t>((nvec + 255) / 256, 8192);
+  hipLaunchKernelGGL(gn_apply_pad_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const half_t*)a->src0,
+                     (const half_t*)a->src1, a->c_split, a->ld0, a->ld1, h, w, pad, a->channels, a->scale, a->shift,
+                     silu, (half_t*)y, ld_y, nvec);
+  return check_launch("gn_apply_pad");
 }
 
 extern "C" int sdk_layer_norm(const void* x, void* y, int32_t rows, int32_t cols, int32_t ld_x, int32_t ld_y,

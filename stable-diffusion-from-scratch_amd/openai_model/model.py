@@ -138,15 +138,17 @@ class ResBlock(TimestepBlock):
                 self._pc_skip = ops.PackedConv([(sk.weight, self.channels)], sk.bias, device=dev)
 
     def _run(self, x, emb_all, emb_off):
-        xa = ops.group_norm_apply(x, self.in_layers[0].stats(x), silu=True)
-        h = ops.conv2d(self._pc1, xa, row_bias=(emb_all, emb_off))
-        ha = ops.group_norm_apply(h, self.out_layers[0].stats(h), silu=True)
+        # GN+SiLU outputs are written zero-bordered: both 3x3 convs run with pad 0 (mask-free gather)
+        gp, cp = ops.gn_conv_pad()
+        xa = ops.group_norm_apply(x, self.in_layers[0].stats(x), silu=True, pad=gp)
+        h = ops.conv2d(self._pc1, xa, pad=cp, row_bias=(emb_all, emb_off))
+        ha = ops.group_norm_apply(h, self.out_layers[0].stats(h), silu=True, pad=gp)
         if self._skip_mode == "identity":
-            return ops.conv2d(self._pc2, ha, residual=x)
+            return ops.conv2d(self._pc2, ha, pad=cp, residual=x)
         if self._skip_mode == "fused":
-            return ops.conv2d(self._pc2, ha, seg2=(x, None, False))
+            return ops.conv2d(self._pc2, ha, pad=cp, seg2=(x, None, False))
         skip = ops.conv2d(self._pc_skip, x)
-        return ops.conv2d(self._pc2, ha, residual=skip)
+        return ops.conv2d(self._pc2, ha, pad=cp, residual=skip)
 
 
 class UNetModel(nn.Module):
@@ -344,6 +346,7 @@ class UNetModel(nn.Module):
         h = self.middle_block._run(h, st)
         for module in self.output_blocks:
             h = module._run((h, hs.pop()), st)
-        ha = ops.group_norm_apply(h, self.out[0].stats(h), silu=True)
-        out = ops.conv2d(self._pc_out, ha, out_mode=ops.OUT_NCHW_F32)
+        gp, cp = ops.gn_conv_pad()
+        ha = ops.group_norm_apply(h, self.out[0].stats(h), silu=True, pad=gp)
+        out = ops.conv2d(self._pc_out, ha, pad=cp, out_mode=ops.OUT_NCHW_F32)
         return out if x.dtype == torch.float32 else out.to(x.dtype)

@@ -368,14 +368,29 @@ def _gn_args(x):
     return args, (B, H, W, Ch), a0.device
 
 
-def group_norm_apply(x, gn, silu=True, out=None):
-    """y = silu?(x*scale + shift) — the normalised (possibly concatenated) input, contiguous NHWC."""
+# zero-bordered GN+SiLU outputs for pad-0 3x3 convs (mask-free gather); 0 = the masked pad-1 path
+PREPAD = 1
+
+
+def gn_conv_pad():
+    """(pad written by group_norm_apply, pad of the 3x3 conv that consumes it)."""
+    return (1, 0) if PREPAD else (0, 1)
+
+
+def group_norm_apply(x, gn, silu=True, out=None, pad=0):
+    """y = silu?(x*scale + shift) — the normalised (possibly concatenated) input, contiguous NHWC.
+    ``pad`` > 0 writes it into a zero-bordered [B, H+2pad, W+2pad, C] image for a pad-0 3x3 conv."""
     args, (B, H, W, Ch), dev = _gn_args(x)
     args.scale, args.shift = gn[0].data_ptr(), gn[1].data_ptr()
-    y = out if out is not None else torch.empty(B, H, W, Ch, dtype=torch.float16, device=dev)
+    y = out if out is not None else torch.empty(B, H + 2 * pad, W + 2 * pad, Ch, dtype=torch.float16, device=dev)
     if PROFILER.active:
         PROFILER.begin("gn_apply", None)
-    check(lib().sdk_group_norm_apply(C.byref(args), 1 if silu else 0, _ptr(y), Ch, _stream()), "group_norm_apply")
+    if pad:
+        check(lib().sdk_group_norm_apply_padded(C.byref(args), 1 if silu else 0, _ptr(y), Ch, H, W, pad, _stream()),
+              "group_norm_apply_padded")
+    else:
+        check(lib().sdk_group_norm_apply(C.byref(args), 1 if silu else 0, _ptr(y), Ch, _stream()),
+              "group_norm_apply")
     if PROFILER.active:
         PROFILER.end()
     return y

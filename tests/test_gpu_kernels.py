@@ -286,6 +286,26 @@ def test_nchw_to_nhwc(ops):
     assert torch.equal(y.cpu(), ref.half())
 
 
+@pytest.mark.parametrize("H,W,C,pad", [(64, 64, 320, 1), (9, 7, 64, 1), (16, 16, 1280, 2)])
+def test_group_norm_apply_padded(ops, H, W, C, pad):
+    """Zero-bordered GN+SiLU output == F.pad of the unpadded output; a pad-0 3x3 conv over it ==
+    the pad-1 conv over the unpadded output (the ResBlock fast path)."""
+    x = _rand(2, H, W, C, seed=61).to(DEV)
+    g = torch.rand(C, device=DEV) + 0.5
+    b = torch.randn(C, device=DEV) * 0.1
+    st = ops.group_norm_affine(x, g, b, 1e-5)
+    y0 = ops.group_norm_apply(x, st, silu=True)
+    yp = ops.group_norm_apply(x, st, silu=True, pad=pad)
+    assert yp.shape == (2, H + 2 * pad, W + 2 * pad, C)
+    ref = F.pad(y0.permute(0, 3, 1, 2), (pad, pad, pad, pad)).permute(0, 2, 3, 1)
+    assert torch.equal(yp, ref)
+    if pad == 1:
+        w = torch.randn(C, C, 3, 3) / math.sqrt(9 * C)
+        pc = ops.PackedConv([(w, C)], torch.zeros(C), device=DEV)
+        assert torch.equal(ops.conv2d(pc, yp, pad=0, variant=0), ops.conv2d(pc, y0, pad=1, variant=0)) or \
+            rel_l2(ops.conv2d(pc, yp, pad=0), ops.conv2d(pc, y0, pad=1)) < 1e-3
+
+
 @pytest.mark.parametrize("silu", [True, False])
 def test_group_norm_apply_concat(ops, silu):
     B, H, W, C1, C2 = 2, 16, 16, 640, 320

@@ -6,6 +6,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 SHAPES = [  # (name, B, H, W, Cin, Cout, k, stride, upsample, geglu)
     ("unet64_320x320_3x3", 16, 64, 64, 320, 320, 3, 1, False, 0),
+    ("unet64_320x320_3x3_prepad", 16, 66, 66, 320, 320, 3, 1, False, 0),
+    ("unet16_1280x1280_3x3_prepad", 16, 18, 18, 1280, 1280, 3, 1, False, 0),
+    ("vae128_512x512_3x3_prepad", 16, 130, 130, 512, 512, 3, 1, False, 0),
     ("unet64_640x320_3x3", 16, 64, 64, 640, 320, 3, 1, False, 0),
     ("unet32_640x640_3x3", 16, 32, 32, 640, 640, 3, 1, False, 0),
     ("unet16_1280x1280_3x3", 16, 16, 16, 1280, 1280, 3, 1, False, 0),
@@ -44,7 +47,8 @@ def child():
         w = torch.randn(Co, Ci, k, k, device="cuda") / (Ci * k * k) ** 0.5
         pc = ops.PackedConv([(w, Ci)], torch.zeros(Co, device="cuda"), geglu=bool(geglu), device="cuda")
         mode = ops.OUT_GEGLU_F16 if geglu else ops.OUT_NHWC_F16
-        f = lambda: ops.conv2d(pc, x, stride=st, pad=k // 2, upsample=up, out_mode=mode)
+        pad = 0 if name.endswith("_prepad") else k // 2
+        f = lambda: ops.conv2d(pc, x, stride=st, pad=pad, upsample=up, out_mode=mode)
         y = f()
         torch.cuda.synchronize()
         ts = []
