@@ -8,7 +8,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsdk_amd.so")
+# SD_AMD_LIB selects another build of the same ABI (A/B benchmarking of kernel revisions only)
+LIB_PATH = os.environ.get("SD_AMD_LIB") or os.path.join(_HERE, "libsdk_amd.so")
 
 vp = C.c_void_p
 i32 = C.c_int32

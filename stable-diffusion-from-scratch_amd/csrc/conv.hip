@@ -517,19 +517,26 @@ __device__ __forceinline__ void epilogue_direct(const Params& p, f16v (&acc)[FM]
 constexpr int EPI_RS = 72;                 // scratch row stride (halfs) = 144 B
 constexpr int EPI_BYTES = 32 * EPI_RS * 2;  // per-wave scratch
 
+// Bias and the timestep-embedding row (row_bias of the tile's image) are staged in LDS once per
+// workgroup (stage_epi_vectors, before the K loop): the epilogue reads them with ds_read instead of
+// waiting on a global load per 32-row block.  ``bias_s`` / ``rb_s`` = nullptr fall back to global.
+// Residual rows are loaded one block ahead (issued before the current block's LDS round trip).
 template <int FM, int FN>
 __device__ __forceinline__ void epilogue_lds(const Params& p, f16v (&acc)[FM][FN], int m0, int n0, int m_w, int n_w,
-                                             half_t* wbuf) {
+                                             half_t* wbuf, const float* bias_s = nullptr,
+                                             const float* rb_s = nullptr) {
   const int lane = threadIdx.x & 63;
   const int fr = lane & 31, fh = lane >> 5;
   const bool rb_vec = p.row_bias && !((uintptr_t)p.row_bias & 15) && !(p.rb_ld & 3);
+  half_t* out = reinterpret_cast<half_t*>(p.out);
+  auto bias4 = [&](int n) __attribute__((always_inline)) {
+    return bias_s ? *reinterpret_cast<const f4*>(bias_s + (n - n0)) : *reinterpret_cast<const f4*>(p.bias + n);
+  };
+  if (p.out_mode == SDK_OUT_GEGLU_F16) {
 #pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    const int mt = m0 + m_w + i * 32;       // first pixel of the block (wave-uniform)
-    if (mt >= p.M) continue;
-    const int mw = min(mt + fr, p.M - 1);   // the writer lane's pixel (clamped: its row is never stored)
-    const int bw = mw / p.hw_out;
-    if (p.out_mode == SDK_OUT_GEGLU_F16) {
+    for (int i = 0; i < FM; ++i) {
+      const int mt = m0 + m_w + i * 32;
+      if (mt >= p.M) continue;
 #pragma unroll
       for (int jp = 0; jp < FN / 2; ++jp) {
         const int nob = (n0 + n_w) / 2 + jp * 32;   // first output channel of the block
@@ -539,8 +546,8 @@ __device__ __forceinline__ void epilogue_lds(const Params& p, f16v (&acc)[FM][FN
           const int nx = n0 + n_w + jp * 64 + 8 * g + 4 * fh;
           f4 bx = {0.f, 0.f, 0.f, 0.f}, bg = {0.f, 0.f, 0.f, 0.f};
           if (p.bias) {
-            bx = *reinterpret_cast<const f4*>(p.bias + nx);
-            bg = *reinterpret_cast<const f4*>(p.bias + nx + 32);
+            bx = bias4(nx);
+            bg = bias4(nx + 32);
           }
           h4 o;
 #pragma unroll
@@ -562,17 +569,49 @@ __device__ __forceinline__ void epilogue_lds(const Params& p, f16v (&acc)[FM][FN
 #pragma unroll
               for (int q = 0; q < 8; ++q) v[q] = (half_t)((float)v[q] + (float)rr[q]);
             }
-            *reinterpret_cast<h8*>(reinterpret_cast<half_t*>(p.out) + (size_t)m * p.out_ld + no) = v;
+            *reinterpret_cast<h8*>(out + (size_t)m * p.out_ld + no) = v;
           }
         }
       }
-      continue;
     }
+    return;
+  }
+  // fp16 NHWC: blocks (i, jp) of 32 pixels x (32|64) channels, flattened so the residual rows of
+  // block q+1 are in flight while block q makes its LDS round trip
+  constexpr int NJP = (FN + 1) / 2, NBLK = FM * NJP;
+  h8 rcur[4], rnext[4];
+  auto block_geom = [&](int q, int& mt, int& nb, int& nt) __attribute__((always_inline)) {
+    const int i = q / NJP, jp = (q - i * NJP) * 2;
+    mt = m0 + m_w + i * 32;
+    nb = n0 + n_w + jp * 32;
+    nt = (FN - jp >= 2) ? 2 : 1;
+  };
+  auto load_res = [&](int q, h8 (&rr)[4]) __attribute__((always_inline)) {
+    int mt, nb, nt;
+    block_geom(q, mt, nb, nt);
+    const int lpr = nt * 4, rpi = 64 / lpr;
 #pragma unroll
-    for (int jp = 0; jp < FN; jp += 2) {
-      const int nt = (FN - jp >= 2) ? 2 : 1;      // 32-channel tiles in this block
-      const int nb = n0 + n_w + jp * 32;          // first channel of the block
-      if (nb >= p.N) continue;
+    for (int r = 0; r < 4; ++r) {
+      rr[r] = h8{};
+      if (r >= 2 * nt) continue;
+      const int m = mt + r * rpi + lane / lpr, n = nb + (lane % lpr) * 8;
+      if (m < p.M && n < p.N) rr[r] = *reinterpret_cast<const h8*>(p.res + (size_t)m * p.res_ld + n);
+    }
+  };
+  // one block ahead when the accumulators leave room (<= 96 VGPRs with the prefetch), else the
+  // block's own residual rows are issued before its LDS round trip
+  constexpr bool AHEAD = FM * FN * 16 + 32 <= 96;
+  if (p.res && AHEAD) load_res(0, rcur);
+#pragma unroll
+  for (int q = 0; q < NBLK; ++q) {
+    int mt, nb, nt;
+    block_geom(q, mt, nb, nt);
+    const int i = q / NJP, jp = (q - i * NJP) * 2;
+    if (p.res && AHEAD && q + 1 < NBLK) load_res(q + 1, rnext);
+    if (p.res && !AHEAD) load_res(q, rcur);
+    if (mt < p.M && nb < p.N) {
+      const int mw = min(mt + fr, p.M - 1);   // the writer lane's pixel (clamped: its row is never stored)
+      const int bw = mw / p.hw_out;
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) {
         if (jj >= nt) continue;
@@ -581,28 +620,34 @@ __device__ __forceinline__ void epilogue_lds(const Params& p, f16v (&acc)[FM][FN
           const int n = nb + jj * 32 + 8 * g + 4 * fh;
           float v[4];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] = acc[i][jp + jj][4 * g + q];
+          for (int qq = 0; qq < 4; ++qq) v[qq] = acc[i][jp + jj][4 * g + qq];
           if (n < p.N) {                          // N % 8 == 0 in this mode
             if (p.bias) {
-              const f4 bb = *reinterpret_cast<const f4*>(p.bias + n);
+              const f4 bb = bias4(n);
 #pragma unroll
-              for (int q = 0; q < 4; ++q) v[q] += bb[q];
+              for (int qq = 0; qq < 4; ++qq) v[qq] += bb[qq];
             }
             if (p.row_bias) {
-              const float* rb = p.row_bias + (size_t)bw * p.rb_ld + n;
-              if (rb_vec) {
-                const f4 r4 = *reinterpret_cast<const f4*>(rb);
+              if (rb_s) {
+                const f4 r4 = *reinterpret_cast<const f4*>(rb_s + (n - n0));
 #pragma unroll
-                for (int q = 0; q < 4; ++q) v[q] += r4[q];
+                for (int qq = 0; qq < 4; ++qq) v[qq] += r4[qq];
               } else {
+                const float* rb = p.row_bias + (size_t)bw * p.rb_ld + n;
+                if (rb_vec) {
+                  const f4 r4 = *reinterpret_cast<const f4*>(rb);
 #pragma unroll
-                for (int q = 0; q < 4; ++q) v[q] += rb[q];
+                  for (int qq = 0; qq < 4; ++qq) v[qq] += r4[qq];
+                } else {
+#pragma unroll
+                  for (int qq = 0; qq < 4; ++qq) v[qq] += rb[qq];
+                }
               }
             }
           }
           h4 o;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) o[q] = (half_t)act_fn(p.act, v[q]);
+          for (int qq = 0; qq < 4; ++qq) o[qq] = (half_t)act_fn(p.act, v[qq]);
           *reinterpret_cast<h4*>(wbuf + fr * EPI_RS + jj * 32 + 8 * g + 4 * fh) = o;
         }
       }
@@ -616,13 +661,16 @@ __device__ __forceinline__ void epilogue_lds(const Params& p, f16v (&acc)[FM][FN
         const int m = mt + row, n = nb + c8 * 8;
         if (m < p.M && n < p.N) {
           if (p.res) {
-            const h8 rr = *reinterpret_cast<const h8*>(p.res + (size_t)m * p.res_ld + n);
 #pragma unroll
-            for (int q = 0; q < 8; ++q) v[q] = (half_t)((float)v[q] + (float)rr[q]);
+            for (int qq = 0; qq < 8; ++qq) v[qq] = (half_t)((float)v[qq] + (float)rcur[r][qq]);
           }
-          *reinterpret_cast<h8*>(reinterpret_cast<half_t*>(p.out) + (size_t)m * p.out_ld + n) = v;
+          *reinterpret_cast<h8*>(out + (size_t)m * p.out_ld + n) = v;
         }
       }
+    }
+    if (p.res && AHEAD && q + 1 < NBLK) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) rcur[r] = rnext[r];
     }
   }
 }
@@ -636,11 +684,31 @@ __device__ __forceinline__ void epilogue_lds(const Params& p, f16v (&acc)[FM][FN
 constexpr int EPG_RS = 72;                          // scratch row stride (halfs) = 144 B
 constexpr int EPG_BYTES = 16 * EPG_RS * 2;          // per-wave scratch
 
+// residual rows of one group (16 pixels x 16*NB channels) in read-back order
 template <int NB>
-__device__ __forceinline__ void epi16_group(const Params& p, const f4* a, int mt, int nb, int bw, bool rb_vec,
-                                            half_t* wbuf) {
+__device__ __forceinline__ void epi16_load_res(const Params& p, int mt, int nb, h8 (&rr)[2]) {
+  const int lane = threadIdx.x & 63;
+  constexpr int LPR = NB * 2, RPI = 64 / LPR;
+  const bool geglu = p.out_mode == SDK_OUT_GEGLU_F16;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    rr[r] = h8{};
+    if (geglu ? r > 0 : r >= 16 / RPI) continue;
+    const int row = geglu ? (lane >> 2) : r * RPI + lane / LPR;
+    const int n = geglu ? nb / 2 + (lane & 3) * 8 : nb + (lane % LPR) * 8;
+    const int m = mt + row;
+    if (m < p.M && n < (geglu ? p.N / 2 : p.N)) rr[r] = *reinterpret_cast<const h8*>(p.res + (size_t)m * p.res_ld + n);
+  }
+}
+
+template <int NB>
+__device__ __forceinline__ void epi16_group(const Params& p, const f4* a, int mt, int nb, int n0, int bw, bool rb_vec,
+                                            half_t* wbuf, const float* bias_s, const float* rb_s, const h8 (&rr)[2]) {
   const int lane = threadIdx.x & 63, px = lane & 15, cg = lane >> 4;
   half_t* out = reinterpret_cast<half_t*>(p.out);
+  auto bias4 = [&](int n) __attribute__((always_inline)) {
+    return bias_s ? *reinterpret_cast<const f4*>(bias_s + (n - n0)) : *reinterpret_cast<const f4*>(p.bias + n);
+  };
   if (p.out_mode == SDK_OUT_GEGLU_F16) {            // NB == 4: blocks 0,1 = x rows, 2,3 = gate rows
     const int nob = nb / 2;
     if (nob >= p.N / 2) return;
@@ -649,8 +717,8 @@ __device__ __forceinline__ void epi16_group(const Params& p, const f4* a, int mt
       const int nx = nb + 16 * j + 4 * cg;
       f4 bx = {0.f, 0.f, 0.f, 0.f}, bg = {0.f, 0.f, 0.f, 0.f};
       if (p.bias) {
-        bx = *reinterpret_cast<const f4*>(p.bias + nx);
-        bg = *reinterpret_cast<const f4*>(p.bias + nx + 32);
+        bx = bias4(nx);
+        bg = bias4(nx + 32);
       }
       h4 o;
 #pragma unroll
@@ -662,9 +730,8 @@ __device__ __forceinline__ void epi16_group(const Params& p, const f4* a, int mt
     const int m = mt + row, no = nob + c8 * 8;
     if (m < p.M && no < p.N / 2) {
       if (p.res) {
-        const h8 rr = *reinterpret_cast<const h8*>(p.res + (size_t)m * p.res_ld + no);
 #pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = (half_t)((float)v[q] + (float)rr[q]);
+        for (int q = 0; q < 8; ++q) v[q] = (half_t)((float)v[q] + (float)rr[0][q]);
       }
       *reinterpret_cast<h8*>(out + (size_t)m * p.out_ld + no) = v;
     }
@@ -679,19 +746,25 @@ __device__ __forceinline__ void epi16_group(const Params& p, const f4* a, int mt
     for (int q = 0; q < 4; ++q) v[q] = a[j][q];
     if (n < p.N) {                                  // N % 8 == 0 in this mode
       if (p.bias) {
-        const f4 bb = *reinterpret_cast<const f4*>(p.bias + n);
+        const f4 bb = bias4(n);
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] += bb[q];
       }
       if (p.row_bias) {
-        const float* rb = p.row_bias + (size_t)bw * p.rb_ld + n;
-        if (rb_vec) {
-          const f4 r4 = *reinterpret_cast<const f4*>(rb);
+        if (rb_s) {
+          const f4 r4 = *reinterpret_cast<const f4*>(rb_s + (n - n0));
 #pragma unroll
           for (int q = 0; q < 4; ++q) v[q] += r4[q];
         } else {
+          const float* rb = p.row_bias + (size_t)bw * p.rb_ld + n;
+          if (rb_vec) {
+            const f4 r4 = *reinterpret_cast<const f4*>(rb);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] += rb[q];
+            for (int q = 0; q < 4; ++q) v[q] += r4[q];
+          } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] += rb[q];
+          }
         }
       }
     }
@@ -708,28 +781,48 @@ __device__ __forceinline__ void epi16_group(const Params& p, const f4* a, int mt
     const int m = mt + row, n = nb + c8 * 8;
     if (m < p.M && n < p.N) {
       if (p.res) {
-        const h8 rr = *reinterpret_cast<const h8*>(p.res + (size_t)m * p.res_ld + n);
 #pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = (half_t)((float)v[q] + (float)rr[q]);
+        for (int q = 0; q < 8; ++q) v[q] = (half_t)((float)v[q] + (float)rr[r][q]);
       }
       *reinterpret_cast<h8*>(out + (size_t)m * p.out_ld + n) = v;
     }
   }
 }
 
+// groups (i, g) flattened; the residual rows of group q+1 are loaded while group q is written
 template <int FM, int FN>
 __device__ __forceinline__ void epilogue16_tile(const Params& p, f4 (&acc)[FM][FN], int m0, int n0, int m_w, int n_w,
-                                                half_t* wbuf) {
+                                                half_t* wbuf, const float* bias_s = nullptr,
+                                                const float* rb_s = nullptr) {
   const int lane = threadIdx.x & 63, px = lane & 15;
   const bool rb_vec = p.row_bias && !((uintptr_t)p.row_bias & 15) && !(p.rb_ld & 3);
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
+  constexpr int NG = FN / 4 + (FN % 4 == 2 ? 1 : 0), NQ = FM * NG;
+  constexpr bool AHEAD = FM * FN * 4 + 16 <= 96;
+  h8 rcur[2], rnext[2];
+  auto load = [&](int q, h8 (&rr)[2]) __attribute__((always_inline)) {
+    const int i = q / NG, g = q - i * NG;
     const int mt = m0 + m_w + 16 * i;
-    if (mt >= p.M) continue;
-    const int bw = min(mt + px, p.M - 1) / p.hw_out;
+    if (g < FN / 4) epi16_load_res<4>(p, mt, n0 + n_w + 64 * g, rr);
+    else epi16_load_res<2>(p, mt, n0 + n_w + 16 * (FN - 2), rr);
+  };
+  if (p.res && AHEAD) load(0, rcur);
 #pragma unroll
-    for (int g = 0; g < FN / 4; ++g) epi16_group<4>(p, &acc[i][4 * g], mt, n0 + n_w + 64 * g, bw, rb_vec, wbuf);
-    if constexpr (FN % 4 == 2) epi16_group<2>(p, &acc[i][FN - 2], mt, n0 + n_w + 16 * (FN - 2), bw, rb_vec, wbuf);
+  for (int q = 0; q < NQ; ++q) {
+    const int i = q / NG, g = q - i * NG;
+    if (p.res && AHEAD && q + 1 < NQ) load(q + 1, rnext);
+    if (p.res && !AHEAD) load(q, rcur);
+    const int mt = m0 + m_w + 16 * i;
+    if (mt < p.M) {
+      const int bw = min(mt + px, p.M - 1) / p.hw_out;
+      if (g < FN / 4)
+        epi16_group<4>(p, &acc[i][4 * g], mt, n0 + n_w + 64 * g, n0, bw, rb_vec, wbuf, bias_s, rb_s, rcur);
+      else
+        epi16_group<2>(p, &acc[i][FN - 2], mt, n0 + n_w + 16 * (FN - 2), n0, bw, rb_vec, wbuf, bias_s, rb_s, rcur);
+    }
+    if (p.res && AHEAD && q + 1 < NQ) {
+      rcur[0] = rnext[0];
+      rcur[1] = rnext[1];
+    }
   }
 }
 
@@ -795,9 +888,11 @@ struct Cfg {
   static constexpr int GPW = (NINSTR + NW - 1) / NW;     // pieces per wave (padded: the same count in
                                                          // every wave keeps the vmcnt immediate exact)
   static_assert(TBM % 8 == 0 && TBN % 8 == 0, "A/B boundary must align to an 8-row piece");
-  static constexpr int LDS_BYTES = NS * STAGE_H * 2 + (GPW * NW > NINSTR ? 1024 : 0);  // + dummy slot
+  static constexpr int RING_BYTES = NS * STAGE_H * 2 + (GPW * NW > NINSTR ? 1024 : 0);  // + dummy slot
+  static constexpr int LDS_BYTES = RING_BYTES + 2 * TBN * 4;   // + staged bias / embedding row
   static_assert(LDS_BYTES <= 160 * 1024, "the ring must fit the 160 KiB LDS");
-  static_assert(LDS_BYTES / NW >= EPI_BYTES, "per-wave epilogue scratch");
+  static_assert(RING_BYTES / NW >= EPI_BYTES, "per-wave epilogue scratch");
+  static_assert(TBN <= NT, "one staged bias element per thread");
 };
 
 #define SDK_SEGF(f) (s1 ? p.seg[1].f : p.seg[0].f)
@@ -936,6 +1031,35 @@ __device__ __forceinline__ void dma_a_piece(const Params& p, const DmaSrc& d, ha
   }
 }
 
+// Epilogue vectors of a tile, loaded into registers before the K loop (one element per thread,
+// tid < tbn) and written to LDS after it: bias[n0 + tid] and, when the tile's rows lie in one
+// image, that image's embedding row row_bias[b][n0 + tid].
+struct EpiVec {
+  float bias, rb;
+  bool one_img;
+};
+
+__device__ __forceinline__ EpiVec epi_vec_load(const Params& p, int m0, int n0, int tbm, int tbn) {
+  const int tid = threadIdx.x;
+  EpiVec e{0.f, 0.f, false};
+  const int b0 = m0 / p.hw_out;
+  e.one_img = p.row_bias && p.split == 1 && b0 == (min(m0 + tbm, p.M) - 1) / p.hw_out;
+  if (tid < tbn && n0 + tid < p.N) {
+    if (p.bias) e.bias = p.bias[n0 + tid];
+    if (e.one_img) e.rb = p.row_bias[(size_t)b0 * p.rb_ld + n0 + tid];
+  }
+  return e;
+}
+
+__device__ __forceinline__ void epi_vec_store(const EpiVec& e, float* vec_s, int tbn) {
+  const int tid = threadIdx.x;
+  if (tid < tbn) {
+    vec_s[tid] = e.bias;
+    vec_s[tbn + tid] = e.rb;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
 // One (tile, K-split) work item per workgroup, two LDS stages.
 template <class CF>
 __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_glds_kernel(Params p) {
@@ -967,6 +1091,7 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_glds_kernel(Params p)
     cx[j] = x;
     cy[j] = y;
   }
+  const EpiVec ev = epi_vec_load(p, m0, n0, CF::TBM, CF::TBN);
   int sg, ky, kx, cb;
   ph_kstate(p, kt0, sg, ky, kx, cb);
   // K-steps past kt1 still issue their pieces (zero-page DMAs into the idle stage) so every
@@ -1066,18 +1191,22 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_glds_kernel(Params p)
 #undef SDK_STAGE
   // the trailing zero-page DMAs land before the ring is reused as epilogue scratch
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float* vec_s = reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + CF::RING_BYTES);
+  epi_vec_store(ev, vec_s, CF::TBN);
   __builtin_amdgcn_s_barrier();
+  const float* bias_s = p.bias ? vec_s : nullptr;
+  const float* rb_s = ev.one_img ? vec_s + CF::TBN : nullptr;
   if constexpr (CF::M16) {
     if (p.split == 1 && (p.out_mode == SDK_OUT_NHWC_F16 || p.out_mode == SDK_OUT_GEGLU_F16))
       epilogue16_tile<CF::FM16, CF::FN16>(p, acc16, m0, n0, wm * CF::TM, wn * CF::TN,
-                                          lds + wave * (CF::LDS_BYTES / CF::NW / 16 * 8));
+                                          lds + wave * (CF::RING_BYTES / CF::NW / 16 * 8), bias_s, rb_s);
     else
       epilogue16_tile_direct<CF::FM16, CF::FN16>(p, acc16, m0, n0, wm * CF::TM, wn * CF::TN, sidx);
     return;
   }
   if (p.split == 1 && (p.out_mode == SDK_OUT_NHWC_F16 || p.out_mode == SDK_OUT_GEGLU_F16))
     epilogue_lds<CF::FM, CF::FN>(p, acc, m0, n0, wm * CF::TM, wn * CF::TN,
-                                 lds + wave * (CF::LDS_BYTES / CF::NW / 16 * 8));
+                                 lds + wave * (CF::RING_BYTES / CF::NW / 16 * 8), bias_s, rb_s);
   else
     epilogue_direct<CF::FM, CF::FN>(p, acc, m0, n0, wm * CF::TM, wn * CF::TN, sidx);
 }
@@ -1258,8 +1387,10 @@ __device__ __forceinline__ void epilogue16_direct(const Params& p, f4 (&acc)[4][
 template <int S_, int D_>
 struct PhCfg {
   static constexpr int S = S_, D = D_;
-  static constexpr int LDS_BYTES = S * 128 * BK * 2;
-  static_assert(S >= D + 2 && D >= 2 && LDS_BYTES <= 160 * 1024, "ring too small / too large");
+  static constexpr int RING_BYTES = S * 128 * BK * 2;
+  static constexpr bool VEC = RING_BYTES + 2 * 256 * 4 <= 160 * 1024;   // room for the staged bias / embedding
+  static constexpr int LDS_BYTES = RING_BYTES + (VEC ? 2 * 256 * 4 : 0);
+  static_assert(S >= D + 2 && D >= 2 && RING_BYTES <= 160 * 1024, "ring too small / too large");
 };
 constexpr int PH_HALF = 128 * BK;   // halfs per half-tile slot
 
@@ -1281,6 +1412,7 @@ __global__ void __launch_bounds__(512) conv_ph_kernel(Params p) {
   const int rch = (lane & 7) ^ ((wave * 4 + (lrow >> 1)) & 7);
 
   const DmaSrc d = make_dma_src(p);
+  const EpiVec ev = epi_vec_load(p, m0, n0, 256, 256);
   // this lane's DMA rows: slot row j*64 + wave*8 + lrow of every half (q = half*2 + j)
   unsigned pixb[4], msk[4], wv[4];
   const int mrow = m0 + wave * 8 + lrow;
@@ -1488,7 +1620,11 @@ __global__ void __launch_bounds__(512) conv_ph_kernel(Params p) {
     return;
   }
   // every wave past its last ring read before the ring is reused as epilogue scratch
+  float* vec_s = reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + PC::RING_BYTES);
+  if constexpr (PC::VEC) epi_vec_store(ev, vec_s, 256);
   __builtin_amdgcn_s_barrier();
+  const float* bias_s = (PC::VEC && p.bias) ? vec_s : nullptr;
+  const float* rb_s = (PC::VEC && ev.one_img) ? vec_s + 256 : nullptr;
   if constexpr (M16) {
     if (p.split == 1 && (p.out_mode == SDK_OUT_NHWC_F16 || p.out_mode == SDK_OUT_GEGLU_F16)) {
       epilogue16_lds(p, acc16[0], m0, n0, wr * 64, wc * 64, lds + wave * (EPI16_BYTES / 2));
@@ -1500,8 +1636,8 @@ __global__ void __launch_bounds__(512) conv_ph_kernel(Params p) {
     return;
   }
   if (p.split == 1 && (p.out_mode == SDK_OUT_NHWC_F16 || p.out_mode == SDK_OUT_GEGLU_F16)) {
-    epilogue_lds<2, 2>(p, acc[0], m0, n0, wr * 64, wc * 64, lds + wave * (EPI_BYTES / 2));
-    epilogue_lds<2, 2>(p, acc[1], m0, n0, 128 + wr * 64, wc * 64, lds + wave * (EPI_BYTES / 2));
+    epilogue_lds<2, 2>(p, acc[0], m0, n0, wr * 64, wc * 64, lds + wave * (EPI_BYTES / 2), bias_s, rb_s);
+    epilogue_lds<2, 2>(p, acc[1], m0, n0, 128 + wr * 64, wc * 64, lds + wave * (EPI_BYTES / 2), bias_s, rb_s);
   } else {
     epilogue_direct<2, 2>(p, acc[0], m0, n0, wr * 64, wc * 64, sidx);
     epilogue_direct<2, 2>(p, acc[1], m0, n0, 128 + wr * 64, wc * 64, sidx);

@@ -45,10 +45,15 @@ def child():
     for name, B, H, W, Ci, Co, k, st, up, geglu in SHAPES:
         x = torch.randn(B, H, W, Ci, device="cuda").half()
         w = torch.randn(Co, Ci, k, k, device="cuda") / (Ci * k * k) ** 0.5
-        pc = ops.PackedConv([(w, Ci)], torch.zeros(Co, device="cuda"), geglu=bool(geglu), device="cuda")
+        nob = os.environ.get("BENCH_NO_BIAS") == "1"
+        pc = ops.PackedConv([(w, Ci)], None if nob else torch.zeros(Co, device="cuda"), geglu=bool(geglu),
+                            device="cuda")
         mode = ops.OUT_GEGLU_F16 if geglu else ops.OUT_NHWC_F16
         pad = 0 if name.endswith("_prepad") else k // 2
-        f = lambda: ops.conv2d(pc, x, stride=st, pad=pad, upsample=up, out_mode=mode)
+        resid = None
+        if os.environ.get("BENCH_RESIDUAL") == "1" and not geglu and st == 1 and not up:
+            resid = torch.randn(B, H - 2 * (k // 2 - pad), W - 2 * (k // 2 - pad), Co, device="cuda").half()
+        f = lambda: ops.conv2d(pc, x, stride=st, pad=pad, upsample=up, out_mode=mode, residual=resid)
         y = f()
         torch.cuda.synchronize()
         ts = []
