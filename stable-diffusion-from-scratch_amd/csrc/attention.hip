@@ -62,7 +62,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long lo
   return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
 }
 
-template <int DQK, int DV, int NW, int QB>
+// CAUSAL is a template flag: the SD UNet's non-causal instantiations carry no masking code
+template <int DQK, int DV, int NW, int QB, bool CAUSAL = false>
 __global__ void __launch_bounds__(NW * 64, QB == 2 ? 1 : 2) attn_fwd_kernel(AttnParams p) {
   constexpr int NT = NW * 64;
   constexpr int KLD = DQK + 8;                                       // K row stride (halfs)
@@ -151,7 +152,7 @@ __global__ void __launch_bounds__(NW * 64, QB == 2 ? 1 : 2) attn_fwd_kernel(Attn
 #pragma unroll
   for (int qb = 0; qb < QB; ++qb) { m_run[qb] = 0.f; l_run[qb] = 0.f; negm[qb] = f16v{}; }
   int ntiles = (p.nk + KT - 1) / KT;
-  if (p.causal) {   // tiles past the workgroup's last query row hold only masked keys
+  if constexpr (CAUSAL) {   // tiles past the workgroup's last query row hold only masked keys
     const int qlast = min(p.nq, (int)(blockIdx.x + 1) * (32 * QB * NW)) - 1;
     ntiles = min(ntiles, qlast / KT + 1);
   }
@@ -195,14 +196,24 @@ __global__ void __launch_bounds__(NW * 64, QB == 2 ? 1 : 2) attn_fwd_kernel(Attn
     h8 pf[QB][4];
 #pragma unroll
     for (int qb = 0; qb < QB; ++qb) {
-      const int qrow = q0 + qb * 32 + fr;
-      if (key0 + KT > p.nk || (p.causal && key0 + KT - 1 > q0 + qb * 32)) {   // ragged / diagonal tiles only
+      if constexpr (CAUSAL) {
+        const int qrow = q0 + qb * 32 + fr;
+        if (key0 + KT > p.nk || key0 + KT - 1 > q0 + qb * 32) {   // ragged / diagonal tiles only
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+              if (key >= p.nk || key > qrow) s[qb][kb][r] = -1e30f;
+            }
+        }
+      } else if (key0 + KT > p.nk) {           // ragged last tile only
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
-            if (key >= p.nk || (p.causal && key > qrow)) s[qb][kb][r] = -1e30f;
+            if (key >= p.nk) s[qb][kb][r] = -1e30f;
           }
       }
       float mt = fmaxf(s[qb][0][0], s[qb][0][1]);
@@ -308,6 +319,13 @@ template <int DQK, int DV, int NW, int QB>
 int launch(const AttnParams& p, hipStream_t s) {
   constexpr int ROWS = 32 * QB * NW;
   dim3 grid((p.nq + ROWS - 1) / ROWS, p.heads, p.batch);
+  if (p.causal) {
+    if constexpr (QB == 1) {   // the CLIP text tower's head sizes; other forms are not instantiated
+      hipLaunchKernelGGL((attn_fwd_kernel<DQK, DV, NW, QB, true>), grid, dim3(NW * 64), 0, s, p);
+      return check_launch("attn_fwd_causal");
+    }
+    return fail(SDK_EINVAL, "attention: causal needs the one-block-per-wave form");
+  }
   hipLaunchKernelGGL((attn_fwd_kernel<DQK, DV, NW, QB>), grid, dim3(NW * 64), 0, s, p);
   return check_launch("attn_fwd");
 }

@@ -59,7 +59,9 @@ struct Params {
   int split, kt_per_split;
   int tiles_m, tiles_n;
   int variant;          // 0: register-staged 128x128 (A transforms); 2/3/4: LDS-DMA 256x256 / 256x128 / 128x128
-  int act;              // epilogue activation after bias / embedding, before the residual (sdk_conv_act)
+  int act;              // epilogue activation after bias / embedding, before the residual (sdk_conv_act);
+                        // only the register-staged kernel and the split-K reduce apply it (act forces
+                        // variant 0), so the LDS-DMA kernels' epilogues carry no activation code
   int nomask;           // segment 0 has every tap in range (pad 0, no pad_end / upsample, cin % 64 == 0):
                         // the LDS-DMA A gather is a lane base + a scalar tap offset, no masks
 };
@@ -470,7 +472,7 @@ __device__ __forceinline__ void epilogue_direct(const Params& p, f16v (&acc)[FM]
           }
           h4 o;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) o[q] = (half_t)act_fn(p.act, v[q]);
+          for (int q = 0; q < 4; ++q) o[q] = (half_t)v[q];
           if (p.res) {
             const h4 rr = *reinterpret_cast<const h4*>(p.res + (size_t)m * p.res_ld + n);
 #pragma unroll
@@ -494,7 +496,6 @@ __device__ __forceinline__ void epilogue_direct(const Params& p, f16v (&acc)[FM]
           float x = acc[i][j][4 * g + q];
           if (p.bias) x += p.bias[n + q];
           if (p.row_bias) x += p.row_bias[(size_t)b * p.rb_ld + n + q];
-          x = act_fn(p.act, x);
           if (p.res) x += (float)p.res[(size_t)m * p.res_ld + n + q];
           if (mode == SDK_OUT_NCHW_F32)
             out[((size_t)b * p.N + n + q) * p.hw_out + (m - b * p.hw_out)] = x;
@@ -647,7 +648,7 @@ __device__ __forceinline__ void epilogue_lds(const Params& p, f16v (&acc)[FM][FN
           }
           h4 o;
 #pragma unroll
-          for (int qq = 0; qq < 4; ++qq) o[qq] = (half_t)act_fn(p.act, v[qq]);
+          for (int qq = 0; qq < 4; ++qq) o[qq] = (half_t)v[qq];
           *reinterpret_cast<h4*>(wbuf + fr * EPI_RS + jj * 32 + 8 * g + 4 * fh) = o;
         }
       }
@@ -770,7 +771,7 @@ __device__ __forceinline__ void epi16_group(const Params& p, const f4* a, int mt
     }
     h4 o;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) o[q] = (half_t)act_fn(p.act, v[q]);
+    for (int q = 0; q < 4; ++q) o[q] = (half_t)v[q];
     *reinterpret_cast<h4*>(wbuf + px * EPG_RS + 16 * j + 4 * cg) = o;
   }
   constexpr int LPR = NB * 2, RPI = 64 / LPR;       // lanes per row, rows per instruction
@@ -850,7 +851,6 @@ __device__ __forceinline__ void epilogue16_tile_direct(const Params& p, f4 (&acc
         float x = acc[i][j][q];
         if (p.bias) x += p.bias[n + q];
         if (p.row_bias) x += p.row_bias[(size_t)b * p.rb_ld + n + q];
-        x = act_fn(p.act, x);
         if (p.res) x += (float)p.res[(size_t)m * p.res_ld + n + q];
         if (p.out_mode == SDK_OUT_NCHW_F32)
           out[((size_t)b * p.N + n + q) * p.hw_out + (m - b * p.hw_out)] = x;
@@ -1310,7 +1310,7 @@ __device__ __forceinline__ void epilogue16_lds(const Params& p, f4 (&acc)[4][2][
         }
         h4 o;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) o[q] = (half_t)act_fn(p.act, v[q]);
+        for (int q = 0; q < 4; ++q) o[q] = (half_t)v[q];
         *reinterpret_cast<h4*>(wbuf + px * EPI16_RS + 32 * b + 16 * j + 4 * cg) = o;
       }
     // read back: 16 pixel rows x 64 channels = 8 lanes x 16 B per row, 8 rows per instruction
@@ -1356,7 +1356,6 @@ __device__ __forceinline__ void epilogue16_direct(const Params& p, f4 (&acc)[4][
           float x = acc[i][b2][j][q];
           if (p.bias) x += p.bias[n + q];
           if (p.row_bias) x += p.row_bias[(size_t)b * p.rb_ld + n + q];
-          x = act_fn(p.act, x);
           if (p.res) x += (float)p.res[(size_t)m * p.res_ld + n + q];
           if (p.out_mode == SDK_OUT_NCHW_F32)
             out[((size_t)b * p.N + n + q) * p.hw_out + (m - b * p.hw_out)] = x;
@@ -1795,6 +1794,7 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
       transform = true;
   }
   if ((double)((a->cout + 127) / 128 * 128) * a->k_total * 2 >= 2147483647.0) transform = true;
+  if (a->act != SDK_ACT_NONE) transform = true;   // the CLIP fc1 (once per prompt, not per step)
   // tile configuration: LDS-DMA kernels for transform-free operands, scored by
   // padded-work efficiency x whole-chip wave quantisation x measured per-config
   // throughput

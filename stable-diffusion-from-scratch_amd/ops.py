@@ -191,8 +191,12 @@ class _Autotune:
     SPLITS = (0, 1, 2, 4, 8)
 
     def __init__(self):
+        import os
         self.enabled = False
         self.table = {}
+        ev = os.environ.get("SD_AMD_TUNE_VARIANTS")       # candidate subset (benchmarking the tuner itself)
+        if ev:
+            self.VARIANTS = tuple(int(v) for v in ev.split(","))
 
     def enable(self, on=True):
         self.enabled = on
