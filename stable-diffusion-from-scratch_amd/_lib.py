@@ -73,6 +73,10 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"sd_amd: HIP library not built ({LIB_PATH} missing); run __graft_entry__.build()")
+    # torch first: its HIP runtime (libamdhip64.so.7) is then the one this library binds to.  Loading
+    # the library before torch pulls in a second runtime copy, and its first kernel launch reports
+    # "no ROCm-capable device" once torch has initialised the GPU.
+    import torch  # noqa: F401
     L = C.CDLL(LIB_PATH)
     L.sdk_conv2d_plan.argtypes = [C.POINTER(ConvArgs), C.POINTER(ConvPlanInfo)]
     L.sdk_conv2d.argtypes = [C.POINTER(ConvArgs), vp]
