@@ -149,6 +149,12 @@ int sdk_group_norm_apply(const sdk_group_norm_args* a, int32_t silu, void* y, in
 int sdk_group_norm_apply_padded(const sdk_group_norm_args* a, int32_t silu, void* y, int32_t ld_y, int32_t h,
                                 int32_t w, int32_t pad, sdk_stream_t stream);
 
+/* The post-activation GroupNorm of the DDPM (config C1) UNet (DDPM/models/layers.py:23-38 ConvBlock,
+ * :311-338 ResNetBlock, :154 attention post-norm): y = [silu](x*scale + shift) + post_bias[b][c]
+ * (the time embedding added after block1) + residual[pix][c] (the ResNet skip); both optional. */
+int sdk_group_norm_apply_ex(const sdk_group_norm_args* a, int32_t silu, const float* post_bias, int32_t pb_ld,
+                            const void* residual, int32_t res_ld, void* y, int32_t ld_y, sdk_stream_t stream);
+
 /* ---------------------------------------------------------------- LayerNorm
  * y = (x - mean) * rstd * gamma + beta over the last dim, fp16 in/out, fp32 math.
  * Replaces nn.LayerNorm norm1/2/3 (openai_model/attention.py:216-218,251-253).
@@ -241,6 +247,12 @@ int sdk_extract_patches(const float* z, float* out, int32_t batch, int32_t chann
 int sdk_fold_patches(const float* patches, const float* pix_w, const float* l_w, float* out, int32_t batch,
                      int32_t channels, int32_t h, int32_t w, int32_t ph, int32_t pw, int32_t sy, int32_t sx,
                      int32_t ly, int32_t lx, sdk_stream_t stream);
+
+/* DDPM (C1) UNet glue: F.interpolate(x2, bilinear, align_corners=True) on NHWC fp16
+ * (DDPM/models/layers.py:55-66 UpsampleBlock) and the exact GELU of its time MLP (unet.py:27-32). */
+int sdk_upsample_bilinear2x(const void* x, void* y, int32_t batch, int32_t h, int32_t w, int32_t channels,
+                            sdk_stream_t stream);
+int sdk_gelu(const void* x, void* y, int64_t n, sdk_stream_t stream);
 
 /* ---------------------------------------------------------------- introspection */
 const char* sdk_last_error(void);

@@ -245,6 +245,35 @@ __global__ void __launch_bounds__(256) gn_apply_pad_kernel(const half_t* s0, con
   }
 }
 
+// Post-activation GroupNorm of the DDPM (C1) UNet's ConvBlock / attention block:
+// y = [silu](x*scale + shift) + post_bias[b][c] + residual[pix][c] (either optional).
+__global__ void __launch_bounds__(256) gn_apply_ex_kernel(const half_t* s0, const half_t* s1, int c_split, int ld0,
+                                                          int ld1, int hw, int channels, const float* scale,
+                                                          const float* shift, int silu, const float* pb, int pb_ld,
+                                                          const half_t* res, int res_ld, half_t* y, int ldy,
+                                                          int64_t nvec) {
+  const int c8 = channels / 8;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nvec; e += stride) {
+    const int64_t pix = e / c8;
+    const int c = (int)(e - pix * c8) * 8;
+    const int b = (int)(pix / hw);
+    const h8 v = load_px(s0, s1, c_split, ld0, ld1, (size_t)pix, c);
+    h8 r = {};
+    if (res) r = *reinterpret_cast<const h8*>(res + (size_t)pix * res_ld + c);
+    h8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float x = (float)v[j] * scale[(size_t)b * channels + c + j] + shift[(size_t)b * channels + c + j];
+      if (silu) x = x * __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+      if (pb) x += pb[(size_t)b * pb_ld + c + j];
+      if (res) x += (float)r[j];
+      o[j] = (half_t)x;
+    }
+    *reinterpret_cast<h8*>(y + (size_t)pix * ldy + c) = o;
+  }
+}
+
 // LayerNorm: one wave per row, row cached in registers (cols <= 64*8*MAXV).
 constexpr int LN_MAXV = 4;
 __global__ void __launch_bounds__(256) layer_norm_kernel(const half_t* x, half_t* y, int rows, int cols, int ldx,
@@ -364,6 +393,23 @@ extern "C" int sdk_group_norm_apply_padded(const sdk_group_norm_args* a, int32_t
                      (const half_t*)a->src1, a->c_split, a->ld0, a->ld1, h, w, pad, a->channels, a->scale, a->shift,
                      silu, (half_t*)y, ld_y, nvec);
   return check_launch("gn_apply_pad");
+}
+
+extern "C" int sdk_group_norm_apply_ex(const sdk_group_norm_args* a, int32_t silu, const float* post_bias,
+                                       int32_t pb_ld, const void* residual, int32_t res_ld, void* y, int32_t ld_y,
+                                       sdk_stream_t stream) {
+  if (!a || !a->src0 || !a->scale || !a->shift || !y) return fail(SDK_EINVAL, "group_norm_apply_ex: null pointer");
+  if (a->channels % 8 || a->c_split % 8 || a->c_split <= 0 || a->c_split > a->channels || ld_y % 8 ||
+      ld_y < a->channels || (residual && res_ld % 8))
+    return fail(SDK_EINVAL, "group_norm_apply_ex: channels/c_split/ld_y/res_ld must be multiples of 8");
+  if (a->c_split < a->channels && !a->src1) return fail(SDK_EINVAL, "group_norm_apply_ex: concat without src1");
+  const int64_t nvec = (int64_t)a->batch * a->hw * (a->channels / 8);
+  if (nvec <= 0) return SDK_OK;
+  const int blocks = (int)std::min<int64_t>((nvec + 255) / 256, 8192);
+  hipLaunchKernelGGL(gn_apply_ex_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const half_t*)a->src0,
+                     (const half_t*)a->src1, a->c_split, a->ld0, a->ld1, a->hw, a->channels, a->scale, a->shift,
+                     silu, post_bias, pb_ld, (const half_t*)residual, res_ld, (half_t*)y, ld_y, nvec);
+  return check_launch("gn_apply_ex");
 }
 
 extern "C" int sdk_layer_norm(const void* x, void* y, int32_t rows, int32_t cols, int32_t ld_x, int32_t ld_y,

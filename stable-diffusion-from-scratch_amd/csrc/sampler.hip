@@ -158,6 +158,45 @@ __global__ void __launch_bounds__(128) token_embedding_kernel(const int64_t* ids
   }
 }
 
+// F.interpolate(scale_factor=2, mode="bilinear", align_corners=True) on NHWC fp16, 8 channels per
+// thread: source coordinate = dst * (in - 1) / (out - 1), fp32 weights as torch computes them
+__global__ void __launch_bounds__(256) upsample_bilinear2x_kernel(const half_t* x, half_t* y, int h, int w, int c,
+                                                                  int64_t nvec) {
+  const int c8 = c / 8, ho = 2 * h, wo = 2 * w;
+  const float ry = ho > 1 ? (float)(h - 1) / (float)(ho - 1) : 0.f;
+  const float rx = wo > 1 ? (float)(w - 1) / (float)(wo - 1) : 0.f;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nvec; e += stride) {
+    const int cc = (int)(e % c8) * 8;
+    int64_t r = e / c8;
+    const int ox = (int)(r % wo); r /= wo;
+    const int oy = (int)(r % ho);
+    const int b = (int)(r / ho);
+    const float sy = ry * oy, sx = rx * ox;
+    const int y0 = (int)sy, x0 = (int)sx;
+    const int y1 = min(y0 + 1, h - 1), x1 = min(x0 + 1, w - 1);
+    const float ly = sy - y0, lx = sx - x0, hy = 1.f - ly, hx = 1.f - lx;
+    const half_t* base = x + (size_t)b * h * w * c + cc;
+    const h8 a = *reinterpret_cast<const h8*>(base + ((size_t)y0 * w + x0) * c);
+    const h8 bb = *reinterpret_cast<const h8*>(base + ((size_t)y0 * w + x1) * c);
+    const h8 cq = *reinterpret_cast<const h8*>(base + ((size_t)y1 * w + x0) * c);
+    const h8 d = *reinterpret_cast<const h8*>(base + ((size_t)y1 * w + x1) * c);
+    h8 o;
+    for (int j = 0; j < 8; ++j)
+      o[j] = (half_t)(hy * (hx * (float)a[j] + lx * (float)bb[j]) + ly * (hx * (float)cq[j] + lx * (float)d[j]));
+    *reinterpret_cast<h8*>(y + ((size_t)(b * ho + oy) * wo + ox) * c + cc) = o;
+  }
+}
+
+// exact (erf) GELU, nn.GELU(): fp16 in / out, fp32 math
+__global__ void __launch_bounds__(256) gelu_kernel(const half_t* x, half_t* y, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float v = (float)x[i];
+    y[i] = (half_t)(0.5f * v * (1.0f + erff(v * 0.70710678118654752f)));
+  }
+}
+
 // patch p = ((ly*Lx + lx)*B + b): out[p][c][i][j] = z[b][c][ly*sy + i][lx*sx + j] (torch.nn.Unfold order)
 __global__ void __launch_bounds__(256) extract_patches_kernel(const float* z, float* out, int B, int C, int H, int W,
                                                               int kh, int kw, int sy, int sx, int Lx, int64_t n) {
@@ -208,6 +247,24 @@ __global__ void __launch_bounds__(256) fold_patches_kernel(const float* patches,
 }  // namespace sdk
 
 using namespace sdk;
+
+extern "C" int sdk_upsample_bilinear2x(const void* x, void* y, int32_t batch, int32_t h, int32_t w,
+                                       int32_t channels, sdk_stream_t stream) {
+  if (!x || !y || batch <= 0 || h <= 0 || w <= 0 || channels <= 0 || channels % 8)
+    return fail(SDK_EINVAL, "upsample_bilinear2x: bad args (channels % 8)");
+  const int64_t nvec = (int64_t)batch * 4 * h * w * (channels / 8);
+  const int blocks = (int)std::min<int64_t>((nvec + 255) / 256, 8192);
+  hipLaunchKernelGGL(upsample_bilinear2x_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const half_t*)x,
+                     (half_t*)y, h, w, channels, nvec);
+  return check_launch("upsample_bilinear2x");
+}
+
+extern "C" int sdk_gelu(const void* x, void* y, int64_t n, sdk_stream_t stream) {
+  if (!x || !y || n <= 0) return fail(SDK_EINVAL, "gelu: bad args");
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(gelu_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const half_t*)x, (half_t*)y, n);
+  return check_launch("gelu");
+}
 
 extern "C" int sdk_extract_patches(const float* z, float* out, int32_t batch, int32_t channels, int32_t h, int32_t w,
                                    int32_t kh, int32_t kw, int32_t sy, int32_t sx, sdk_stream_t stream) {

@@ -400,6 +400,47 @@ def group_norm_apply(x, gn, silu=True, out=None, pad=0):
     return y
 
 
+def group_norm_apply_ex(x, gn, silu=True, post_bias=None, residual=None):
+    """y = silu?(x*scale + shift) + post_bias[b, c] + residual (DDPM C1 post-activation GroupNorm)."""
+    args, (B, H, W, Ch), dev = _gn_args(x)
+    args.scale, args.shift = gn[0].data_ptr(), gn[1].data_ptr()
+    y = torch.empty(B, H, W, Ch, dtype=torch.float16, device=dev)
+    pb_ld = 0
+    if post_bias is not None:
+        _need_cuda(post_bias, "group_norm_apply_ex post_bias", torch.float32)
+        pb_ld = post_bias.stride(0)
+    res_ld = 0
+    if residual is not None:
+        _need_cuda(residual, "group_norm_apply_ex residual")
+        res_ld = residual.shape[-1]
+    if PROFILER.active:
+        PROFILER.begin("gn_apply", None)
+    check(lib().sdk_group_norm_apply_ex(C.byref(args), 1 if silu else 0, _ptr(post_bias), pb_ld, _ptr(residual),
+                                        res_ld, _ptr(y), Ch, _stream()), "group_norm_apply_ex")
+    if PROFILER.active:
+        PROFILER.end()
+    return y
+
+
+def upsample_bilinear2x(x):
+    """F.interpolate(scale_factor=2, mode='bilinear', align_corners=True) on NHWC fp16."""
+    _need_cuda(x, "upsample_bilinear2x")
+    x = x.contiguous()
+    B, H, W, Cc = x.shape
+    y = torch.empty(B, 2 * H, 2 * W, Cc, dtype=torch.float16, device=x.device)
+    check(lib().sdk_upsample_bilinear2x(_ptr(x), _ptr(y), B, H, W, Cc, _stream()), "upsample_bilinear2x")
+    return y
+
+
+def gelu(x):
+    """Exact (erf) GELU, fp16."""
+    _need_cuda(x, "gelu")
+    x = x.contiguous()
+    y = torch.empty_like(x)
+    check(lib().sdk_gelu(_ptr(x), _ptr(y), x.numel(), _stream()), "gelu")
+    return y
+
+
 def group_norm_silu(x, gamma, beta, eps, groups=32):
     """GroupNorm + SiLU materialised once (stats pass + apply pass) — the input of a 3x3 conv."""
     return group_norm_apply(x, group_norm_affine(x, gamma, beta, eps, groups), silu=True)

@@ -428,6 +428,44 @@ def gen_ddpm():
                         noises=torch.stack(noises).numpy())
 
 
+def gen_ddpm_unet():
+    """C1: the reference's 58.66 M DDPM UNet (DDPM/models/unet.py) with synthetic
+    weights — one forward at two timesteps, and a 4-step DDPMPipeline.sampling run with it (noise
+    recorded; DDPM/ddpm.py:53-89)."""
+    import importlib
+    sys.path.insert(0, os.path.join(REF, "DDPM"))
+    for k in [k for k in sys.modules if k == "models" or k.startswith("models.")]:
+        del sys.modules[k]
+    unet_mod = importlib.import_module("models.unet")
+    dd = importlib.import_module("ddpm")
+    torch.manual_seed(0)
+    m = unet_mod.UNet(input_channels=3).eval()
+    reinit_(m, 41)
+    g = torch.Generator().manual_seed(42)
+    x = torch.randn(2, 3, 32, 32, generator=g)
+    t = torch.tensor([5, 900])
+    with torch.no_grad():
+        y = m(x, t)
+    pipe = dd.DDPMPipeline(beta_start=1e-4, beta_end=1e-2, num_timesteps=4)
+    x0 = torch.randn(2, 3, 32, 32, generator=g)
+    noises = []
+    real_randn = torch.randn
+
+    def rec_randn(*shape, **kw):
+        z = real_randn(*shape, generator=g)
+        noises.append(z.clone())
+        return z
+
+    torch.randn = rec_randn
+    try:
+        with quiet(), torch.no_grad():
+            img = pipe.sampling(m, x0, "cpu")
+    finally:
+        torch.randn = real_randn
+    np.savez_compressed(os.path.join(OUT, "ddpm_unet.npz"), **sd_keys(m), seed=np.int64(41), x=x.numpy(),
+                        t=t.numpy(), y=y.numpy(), x0=x0.numpy(), out=img.numpy(), noises=torch.stack(noises).numpy())
+
+
 def main():
     install_shims()
     torch.set_num_threads(8)
@@ -441,6 +479,7 @@ def main():
     gen_img2img(fake)
     gen_tiled_decode()
     gen_ddpm()
+    gen_ddpm_unet()
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))

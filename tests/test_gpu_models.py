@@ -318,3 +318,61 @@ def test_fold_patches_vs_torch(sdk, H, W, ph, pw, sy, sx, tie):
     got = ops.extract_patches(zimg.to(DEV), ph, pw, sy, sx).cpu()
     unf = torch.nn.Unfold(kernel_size=(ph, pw), stride=(sy, sx))(zimg).view(B, Cc, ph, pw, -1).permute(4, 0, 1, 2, 3)
     assert torch.equal(got, unf)
+
+
+# ---------------------------------------------------------------- C1 DDPM pixel UNet
+def _ddpm_unet(z):
+    from sd_amd.DDPM.models.unet import UNet
+    m = UNet(input_channels=3)
+    ks = json.loads(bytes(z["keys"]).decode())
+    assert [k for k, _ in ks] == list(m.state_dict().keys())      # reference parameter names / order
+    m.load_state_dict(weights_of(z))
+    return m
+
+
+def test_ddpm_unet_vs_reference(sdk):
+    """The 58.66 M DDPM UNet (5 down / bottleneck / 5 bilinear-up, post-norm attention) on the HIP
+    path vs the reference's own output (golden), B=2, 32x32, t = 5 and 900."""
+    z = load("ddpm_unet")
+    m = _ddpm_unet(z)
+    y = m(torch.from_numpy(z["x"]).to(DEV), torch.from_numpy(z["t"]).to(DEV))
+    assert y.shape == z["y"].shape and y.dtype == torch.float32
+    assert rel_l2(y, torch.from_numpy(z["y"])) < 1e-2
+
+
+def test_ddpm_pipeline_vs_reference(sdk):
+    """DDPMPipeline.sampling (4 steps, the reference's recorded noise) with the HIP UNet."""
+    from sd_amd.DDPM.ddpm import DDPMPipeline
+    z = load("ddpm_unet")
+    m = _ddpm_unet(z)
+    pipe = DDPMPipeline(beta_start=1e-4, beta_end=1e-2, num_timesteps=4)
+    noises = [torch.from_numpy(n) for n in z["noises"]]
+    out = pipe.sampling(m, torch.from_numpy(z["x0"]), DEV, noise_fn=lambda i, shape: noises[i].to(DEV))
+    assert rel_l2(out, torch.from_numpy(z["out"])) < 1e-2
+
+
+def test_ddpm_glue_kernels(sdk):
+    """Bilinear x2 (align_corners=True) vs F.interpolate; exact GELU; post-activation GroupNorm with
+    time-embedding add and residual vs torch."""
+    import torch.nn.functional as F
+    from sd_amd import ops
+    g = torch.Generator().manual_seed(7)
+    for h, w in ((1, 1), (2, 2), (4, 4), (16, 16), (5, 3)):
+        x = torch.randn(2, h, w, 64, generator=g).half()
+        y = ops.upsample_bilinear2x(x.to(DEV)).float().cpu()
+        ref = F.interpolate(x.float().permute(0, 3, 1, 2), scale_factor=2.0, mode="bilinear",
+                            align_corners=True).permute(0, 2, 3, 1)
+        assert y.shape == ref.shape
+        assert (y - ref).abs().max().item() < 2e-2 * max(1.0, ref.abs().max().item())
+    v = torch.randn(4, 512, generator=g).half()
+    assert rel_l2(ops.gelu(v.to(DEV)), F.gelu(v.float())) < 2e-3
+    x = torch.randn(2, 8, 8, 128, generator=g).half().to(DEV)
+    gm, bt = torch.rand(128, device=DEV) + 0.5, torch.randn(128, device=DEV) * 0.1
+    pb = torch.randn(2, 256, generator=g).to(DEV)[:, 64:192]
+    r = torch.randn(2, 8, 8, 128, generator=g).half().to(DEV)
+    st = ops.group_norm_affine(x, gm, bt, 1e-5)
+    y = ops.group_norm_apply_ex(x, st, silu=True, post_bias=pb, residual=r)
+    xf = x.float().permute(0, 3, 1, 2).cpu()
+    ref = F.silu(F.group_norm(xf, 32, gm.cpu(), bt.cpu(), 1e-5)) + pb.cpu()[:, :, None, None]
+    ref = ref.permute(0, 2, 3, 1) + r.float().cpu()
+    assert rel_l2(y, ref) < 3e-3

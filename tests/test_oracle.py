@@ -163,3 +163,27 @@ def test_tiled_decode_vs_reference():
     ref = z["dec"]
     assert dec.shape == ref.shape
     assert np.max(np.abs(dec.numpy() - ref)) <= 1e-4 * max(1.0, np.abs(ref).max())
+
+
+# ---------------------------------------------------------------- C1 DDPM UNet
+def test_ddpm_unet_vs_reference():
+    from oracle import ddpm_ref
+    z = load("ddpm_unet")
+    sd = weights_of(z)
+    y = ddpm_ref.unet_forward(sd, torch.from_numpy(z["x"]), torch.from_numpy(z["t"]))
+    ref = z["y"]
+    assert y.shape == ref.shape
+    assert np.max(np.abs(y.numpy() - ref)) <= 1e-4 * max(1.0, np.abs(ref).max())
+
+
+def test_ddpm_pipeline_with_unet_vs_reference():
+    from oracle import ddpm_ref
+    z = load("ddpm_unet")
+    sd = weights_of(z)
+    tab = sch.ddpm_tables(1e-4, 1e-2, 4)
+    img = z["x0"]
+    noises = list(z["noises"])
+    for t in range(3, -1, -1):
+        eps = ddpm_ref.unet_forward(sd, torch.from_numpy(img), torch.full((img.shape[0],), t)).numpy()
+        img = sch.ddpm_step(img, eps, sch.ddpm_step_scalars(tab, t), noises.pop(0) if t > 0 else None)
+    assert np.max(np.abs(img - z["out"])) <= 1e-4 * max(1.0, np.abs(z["out"]).max())
