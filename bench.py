@@ -39,6 +39,7 @@ CONFIGS = {
     "c3": dict(workload="sd1-txt2img-512-ddim50", unet=SD1_UNET, latent=64, ctx=(77, 768), batch=16),
     "c2": dict(workload="ldm-uncond-256-ddim50", unet=dict(SD1_UNET, use_spatial_transformer=False,
                                                            context_dim=None), latent=32, ctx=None, batch=8),
+    "c1": dict(workload="ddpm-pixel-32-10step", ddpm=True, image=32, batch=4, timesteps=10),
     "c5": dict(workload="sd2shape-768-vpred-ddim50", unet=dict(SD1_UNET, num_heads=-1, num_head_channels=64,
                                                                context_dim=1024), latent=96, ctx=(77, 1024),
                batch=8, v=True),
@@ -100,11 +101,99 @@ def build_models(cfg, device, graph=False):
 
 
 def unet_gflops_per_image(cfg):
-    return {"c3": 803.3, "c2": 125.1, "c5": 2149.1}[cfg]
+    return {"c3": 803.3, "c2": 125.1, "c5": 2149.1, "c1": 3.275}[cfg]
 
 
 def vae_gflops_per_image(cfg):
-    return {"c3": 2514.5, "c2": 622.2, "c5": 5754.3}[cfg]
+    return {"c3": 2514.5, "c2": 622.2, "c5": 5754.3, "c1": 0.0}[cfg]
+
+
+def main_ddpm(args, cfg, world, rank, local, dist, device):
+    """C1 (BASELINE configs[0]): the pixel-space DDPM pipeline, DDPMPipeline.sampling over T steps with the
+    58.66 M DDPM UNet (DDPM/ddpm.py:53-89, DDPM/models/unet.py), one HIP graph per UNet call."""
+    import sd_amd_loader
+    sd_amd_loader.load()
+    from sd_amd import ops
+    from sd_amd import distributed as sdd
+    from sd_amd.DDPM.ddpm import DDPMPipeline
+    from sd_amd.DDPM.models.unet import UNet
+    from sd_amd.graphs import GraphedUNet
+    m = UNet(input_channels=3).to(device)       # (its positional table is a plain tensor: no meta init)
+    synth_init_(m, 1234, device)
+    B, S, T = args.batch or cfg["batch"], cfg["image"], cfg["timesteps"]
+    pipe = DDPMPipeline(beta_start=1e-4, beta_end=1e-2, num_timesteps=T)
+
+    class _Call(torch.nn.Module):       # GraphedUNet's (x, t, context) calling convention
+        def forward(self, x, t, context=None):
+            return m(x, t)
+
+    graphed = GraphedUNet(_Call())
+    model = (lambda x, t: graphed(x, t)) if not args.no_graph else m
+    x_all, _ = sdd.global_inputs(2024, world, B, (3, S, S), None)
+    x0 = sdd.shard(x_all, rank, world).to(device)
+    gen = torch.Generator(device=device).manual_seed(99 + rank)
+    noise_fn = lambda i, shape: torch.randn(shape, device=device, generator=gen)
+    cached = 0
+    if args.tuning_cache and os.path.exists(args.tuning_cache) and not args.no_autotune:
+        cached = ops.AUTOTUNE.load(args.tuning_cache)
+    ops.AUTOTUNE.enable(not args.no_autotune)
+    pipe.sampling(m, x0, device, noise_fn=noise_fn)          # eager: autotune + settle workspaces
+    ops.AUTOTUNE.enable(False)
+
+    def barrier():
+        if dist:
+            import torch.distributed as tdist
+            tdist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(max(args.warmup, 1)):
+        img = pipe.sampling(model, x0, device, noise_fn=noise_fn)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        img = pipe.sampling(model, x0, device, noise_fn=noise_fn)
+    barrier()
+    elapsed = sdd.max_over_ranks(time.perf_counter() - t0, device=device)
+    value = world * B * args.steps / elapsed
+    out = {"metric": METRIC, "value": round(value, 4), "unit": "images/sec", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 3), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "f16",
+           "data": "synthetic (seeded random weights, N(0,1) images and noise)",
+           "config": {"workload": cfg["workload"], "global_batch": world * B, "batch_per_gpu": B,
+                      "image": [3, S, S], "timesteps": T, "parallelism": f"dp{world}", "collective": None},
+           "finite": bool(torch.isfinite(img).all().item()), "hip_graph": not args.no_graph,
+           "tuning_cache_entries": cached}
+    if not args.no_roofline and rank == 0:
+        ops.PROFILER.start()
+        pipe.sampling(m, x0, device, noise_fn=noise_fn)
+        torch.cuda.synchronize()
+        ops.PROFILER.stop()
+        summ = ops.PROFILER.summary()
+        conv = {"launches": 0, "ms": 0.0, "flops": 0.0}
+        for k, d in summ.items():
+            if k.startswith("conv"):
+                for f in conv:
+                    conv[f] += d[f]
+        if conv["launches"]:
+            ach = conv["flops"] / (conv["ms"] / 1000.0) / 1e12
+            out["roofline"] = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
+                               "frac": round(ach / PEAK_F16_TFLOPS, 4), "traffic": None,
+                               "kernel": "conv family (launch-bound at 32x32, B=4)", "launches": conv["launches"],
+                               "avg_launch_us": round(1000 * conv["ms"] / conv["launches"], 2)}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+        from oracle.ddpm_ref import unet_forward
+        torch.set_num_threads(args.cpu_threads)
+        sd = {k: v.detach().float().cpu() for k, v in m.state_dict().items()}
+        xc = torch.randn(1, 3, S, S)
+        t0 = time.perf_counter()
+        unet_forward(sd, xc, torch.tensor([T - 1]))
+        t_unet = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": 1.0 / (T * t_unet), "unit": "images/sec", "cores": args.cpu_threads,
+                               "kind": "port", "sample": f"fp32 CPU oracle: 1 DDPM UNet eval ({t_unet:.2f} s) at "
+                                                         f"batch 1, extrapolated to {T} steps per image"}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
 
 
 def cpu_baseline(cfg_name, cfg, ddim_steps, threads):
@@ -182,6 +271,12 @@ def main():
     device = torch.device("cuda", local if dist else 0)
     torch.cuda.set_device(device)
     cfg = CONFIGS[args.config]
+    if cfg.get("ddpm"):
+        main_ddpm(args, cfg, world, rank, local, dist, device)
+        if dist:
+            import torch.distributed as tdist
+            tdist.destroy_process_group()
+        return
     B = args.batch or cfg["batch"]
     L = cfg["latent"]
 
