@@ -139,6 +139,9 @@ def main_ddpm(args, cfg, world, rank, local, dist, device):
     ops.AUTOTUNE.enable(not args.no_autotune)
     pipe.sampling(m, x0, device, noise_fn=noise_fn)          # eager: autotune + settle workspaces
     ops.AUTOTUNE.enable(False)
+    if args.tuning_out and rank == 0 and len(ops.AUTOTUNE.table) > cached:
+        os.makedirs(os.path.dirname(os.path.abspath(args.tuning_out)), exist_ok=True)
+        ops.AUTOTUNE.save(args.tuning_out)
 
     def barrier():
         if dist:
