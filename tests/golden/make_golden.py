@@ -280,6 +280,37 @@ def gen_vae():
                         cfg=np.frombuffer(json.dumps(TINY_VAE).encode(), dtype=np.uint8))
 
 
+def gen_ddim_cfg(m, cfg):
+    """SURVEY §8(f) rank 1 — classifier-free guidance: the reference DDIMSampler (DDIM/ddim.py:171-178:
+    batch doubled as cat([uc, c]), e = e_u + s·(e_c − e_u)) with the tiny UNet, 4 steps, scale 7.5."""
+    fake = gen_schedule.__fake__
+    ddim_mod = make_ddim_sampler(fake)
+
+    class LD:
+        num_timesteps = 1000
+        alphas_cumprod = fake.alphas_cumprod
+        alphas_cumprod_prev = fake.alphas_cumprod_prev
+        betas = fake.betas
+        device = torch.device("cpu")
+        parameterization = "eps"
+
+        def apply_model(self, x_noisy, t, cond):
+            return m(x_noisy, t, context=torch.cat([cond], 1))
+
+    g = torch.Generator().manual_seed(51)
+    B = 2
+    xT = torch.randn(B, 4, 16, 16, generator=g)
+    c = torch.randn(B, 7, cfg["context_dim"], generator=g)
+    uc = torch.randn(B, 7, cfg["context_dim"], generator=g) * 0.1
+    ddim_mod.noise_like = lambda shape, device, repeat=False: torch.zeros(shape)
+    s = ddim_mod.DDIMSampler(LD())
+    with quiet(), torch.no_grad():
+        samples, _ = s.sample(S=4, batch_size=B, shape=(4, 16, 16), conditioning=c, eta=0.0, x_T=xT,
+                              verbose=False, unconditional_guidance_scale=7.5, unconditional_conditioning=uc)
+    np.savez_compressed(os.path.join(OUT, "ddim_cfg.npz"), xT=xT.numpy(), c=c.numpy(), uc=uc.numpy(),
+                        samples=samples.numpy(), scale=np.float64(7.5), steps=np.int64(4))
+
+
 def gen_img2img(fake):
     """SURVEY §8(f) rank 2 — img2img: AutoEncoderKL.encode → posterior (moments, a recorded-noise
     sample; VAE/autoencoder.py:114-123, Distribution/distribution.py:31-50), DDIMSampler.stochastic_encode
@@ -472,7 +503,8 @@ def main():
     fake = gen_schedule()
     gen_schedule.__fake__ = fake
     gen_ddim_step(fake)
-    gen_unet("unet_tiny", TINY_UNET, 3, with_ctx=True, ddim_steps=4)
+    m_tiny = gen_unet("unet_tiny", TINY_UNET, 3, with_ctx=True, ddim_steps=4)
+    gen_ddim_cfg(m_tiny, TINY_UNET)
     gen_unet("unet_tiny_uncond", TINY_UNET_UNCOND, 5, with_ctx=False)
     gen_unet("unet_tiny_headch", TINY_UNET_HC, 9, with_ctx=True)
     gen_vae()

@@ -376,3 +376,32 @@ def test_ddpm_glue_kernels(sdk):
     ref = F.silu(F.group_norm(xf, 32, gm.cpu(), bt.cpu(), 1e-5)) + pb.cpu()[:, :, None, None]
     ref = ref.permute(0, 2, 3, 1) + r.float().cpu()
     assert rel_l2(y, ref) < 3e-3
+
+
+# ---------------------------------------------------------------- classifier-free guidance
+def test_tiny_ddim_cfg_vs_reference(sdk):
+    """DDIMSampler with unconditional_conditioning + scale 7.5: batch doubled as cat([uc, c]) through the
+    HIP UNet, guidance combined inside the fused DDIM update, vs the reference sampler (golden)."""
+    from sd_amd.openai_model.model import UNetModel
+    from sd_amd.DDIM.ddim import DDIMSampler
+    from sd_amd.DDIM.diffusion_modules import register_schedule
+    u, z = load("unet_tiny"), load("ddim_cfg")
+    m = UNetModel(**cfg_of(u))
+    m.load_state_dict(weights_of(u))
+    sch = register_schedule(1000, 0.00085, 0.012)
+
+    class LD:
+        num_timesteps = 1000
+        alphas_cumprod = sch["alphas_cumprod"]
+        device = torch.device(DEV)
+        parameterization = "eps"
+
+        def apply_model(self, x, t, c):
+            return m(x, t, context=c)
+
+    s = DDIMSampler(LD())
+    out, _ = s.sample(S=int(z["steps"]), batch_size=2, shape=(4, 16, 16), conditioning=torch.from_numpy(z["c"]).to(DEV),
+                      eta=0.0, x_T=torch.from_numpy(z["xT"]).to(DEV), verbose=False,
+                      unconditional_guidance_scale=float(z["scale"]),
+                      unconditional_conditioning=torch.from_numpy(z["uc"]).to(DEV))
+    assert rel_l2(out, torch.from_numpy(z["samples"])) < 1e-2

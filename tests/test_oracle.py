@@ -187,3 +187,18 @@ def test_ddpm_pipeline_with_unet_vs_reference():
         eps = ddpm_ref.unet_forward(sd, torch.from_numpy(img), torch.full((img.shape[0],), t)).numpy()
         img = sch.ddpm_step(img, eps, sch.ddpm_step_scalars(tab, t), noises.pop(0) if t > 0 else None)
     assert np.max(np.abs(img - z["out"])) <= 1e-4 * max(1.0, np.abs(z["out"]).max())
+
+
+# ---------------------------------------------------------------- classifier-free guidance
+def test_ddim_cfg_sampling_vs_reference():
+    from oracle.sampler_ref import ddim_sample
+    z = load("ddim_cfg")
+    u = load("unet_tiny")
+    cfg, sd = cfg_of(u), weights_of(u)
+    c, uc = torch.from_numpy(z["c"]), torch.from_numpy(z["uc"])
+    model = lambda x, t: unet_ref.unet_forward(sd, cfg, x, t, c)
+    uncond = lambda x, t: unet_ref.unet_forward(sd, cfg, x, t, uc)
+    out, _ = ddim_sample(model, torch.from_numpy(z["xT"]), int(z["steps"]), guidance_scale=float(z["scale"]),
+                         uncond_fn=uncond)
+    ref = z["samples"]
+    assert np.max(np.abs(out.numpy() - ref)) <= 1e-4 * max(1.0, np.abs(ref).max())
