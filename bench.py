@@ -389,6 +389,17 @@ def main():
                                "algorithmic_bytes_per_launch": round(conv["bytes"] / conv["launches"]),
                                "traffic_unit": "bytes per launch (PMC, profiles/conv_traffic.json)"}
         out["kernel_time_ms_profiled_step"] = {k: round(v["ms"], 2) for k, v in summ.items()}
+        xa = ops.PROFILER.region_summary("cross_attention")
+        if xa["launches"]:
+            # north-star item: MFMA use of the cross-attention block (to_q + core on the cached
+            # context K/V + to_out with its residual), FLOPs / (its device time x dense peak)
+            ach = xa["flops"] / (xa["ms"] * 1e-3) / 1e12
+            out["cross_attention_block"] = {
+                "achieved": round(ach, 2), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(ach / PEAK_F16_TFLOPS, 4), "ms_per_sample": round(xa["ms"], 2),
+                "share_of_profiled_step": round(xa["ms"] / sum(v["ms"] for v in summ.values()), 4),
+                "by_kind": {k: {"ms": round(v["ms"], 2), "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 1)}
+                            for k, v in xa["by_kind"].items()}}
         if os.environ.get("BENCH_SEQ_OUT"):
             # launch sequence of ONE UNet forward (kind, shape, flops) for tools/trace_step.py,
             # which pairs it with a graph-replayed step of a rocprofv3 trace (device times)

@@ -84,10 +84,15 @@ class CrossAttention(nn.Module):
                 kvx = ops.linear(self._pc_kv, t)
                 k, v, nk = kvx[:, :inner], kvx[:, inner:], N
         else:
+            # cross-attention on the cached context K|V: to_q, the attention core and to_out are
+            # the per-step block the bench reports (``cross_attention_block``)
+            ops.PROFILER.region = "cross_attention"
             q = ops.linear(self._pc_q, t)
             k, v, nk = kv[:, :inner], kv[:, inner:], Lc
         o = ops.attention(q, k, v, batch=B, heads=self.heads, nq=N, nk=nk, head_dim=self.dim_head, scale=self.scale)
-        return ops.linear(self._pc_o, o, residual=residual)
+        out = ops.linear(self._pc_o, o, residual=residual)
+        ops.PROFILER.region = None
+        return out
 
 
 class GELU(nn.Module):

@@ -641,10 +641,13 @@ class _Profiler:
     def __init__(self):
         self.active = False
         self.records = []
+        self.regions = []      # per record: the module region it ran in (None outside any)
+        self.region = None     # set by modules around their launches (e.g. "cross_attention")
         self._cur = None
 
     def start(self):
         self.records = []
+        self.regions = []
         self.active = True
 
     def stop(self):
@@ -668,6 +671,23 @@ class _Profiler:
         e1.record(s)
         kind, variant, flops, e0, shape, nbytes = self._cur
         self.records.append((kind, variant, flops, e0, e1, shape, nbytes))
+        self.regions.append(self.region)
+
+    def region_summary(self, region):
+        """Totals over the launches of one module region: launches, ms, flops, and per kind."""
+        torch.cuda.synchronize()
+        tot = {"launches": 0, "ms": 0.0, "flops": 0.0, "by_kind": {}}
+        for rec, reg in zip(self.records, self.regions):
+            if reg != region:
+                continue
+            kind, _, flops, e0, e1, _, _ = rec
+            ms = e0.elapsed_time(e1)
+            k = tot["by_kind"].setdefault(kind, {"launches": 0, "ms": 0.0, "flops": 0.0})
+            for d in (tot, k):
+                d["launches"] += 1
+                d["ms"] += ms
+                d["flops"] += flops or 0.0
+        return tot
 
     def shape_table(self):
         """Per (kind, shape) totals: launches, ms, TFLOP/s — where the time goes."""
