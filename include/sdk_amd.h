@@ -179,6 +179,27 @@ typedef struct {
 
 int sdk_attention(const sdk_attention_args* a, sdk_stream_t stream);
 
+/* Fused cross-attention block on a cached context K|V: out = (softmax(scale * (t Wq^T)_h K_h^T) V_h)_h
+ * Wo^T + bias + res, one kernel, q and o kept in LDS.  Replaces, per denoising step, the
+ * to_q Linear + flash_attn_func + to_out Linear of CrossAttention.forward with a context
+ * (openai_model/attention.py:63-117) and the residual add of BasicTransformerBlock
+ * (attention.py:249).  t / res / out: [batch*n_img, ld] fp16; kv: [batch*nk, kv_ld] fp16
+ * with K at columns [0, channels) and V at [channels, 2*channels); wq / wo: fp16 [>= channels
+ * rows][w_ld = channels] (row n = output channel); bias fp32 [channels] or NULL.
+ * Shapes: sdk_cross_attention_block_supported() (channels 320 / 640, head_dim 40 / 64 / 80,
+ * nk <= 80, n_img % 64 == 0); others return SDK_EINVAL (callers use the three-launch path).
+ */
+typedef struct {
+  const void* t; const void* kv; const void* wq; const void* wo; const float* bias; const void* res;
+  void* out;
+  int32_t t_ld, kv_ld, w_ld, res_ld, out_ld;
+  int32_t batch, n_img, nk, channels, head_dim;
+  float scale;
+} sdk_xattn_args;
+
+int sdk_cross_attention_block_supported(int32_t channels, int32_t head_dim, int32_t nk, int32_t n_img);
+int sdk_cross_attention_block(const sdk_xattn_args* a, sdk_stream_t stream);
+
 /* ---------------------------------------------------------------- sampler / glue
  * DDIM update (DDIM/ddim.py:194-204 == ldm/diffusion/ddim.py:197-205), fp32,
  * evaluated op by op without contraction so it is bit-identical to torch's CPU

@@ -15,6 +15,7 @@ checkpoints and ``Diffusion/config.yaml`` params load unchanged.  Execution
 """
 from __future__ import annotations
 
+import os
 import math
 
 import torch
@@ -40,6 +41,23 @@ def _gn_stats(gn: nn.GroupNorm, x):
 def _ln_prep(ln: nn.LayerNorm, dev):
     ln._g = ln.weight.detach().to(dev, torch.float32).contiguous()
     ln._b = ln.bias.detach().to(dev, torch.float32).contiguous()
+
+
+# fused to_q + attention + to_out kernel for cross-attention on the cached context (xattn.hip),
+# routed where it measured faster than the three launches (tools/bench_xattn.py, MI355X: 320
+# channels at >= 131072 query rows, e.g. the classifier-free-guidance batch of 2 x 16 at 64x64:
+# 1.11x; level at 65536 rows, slower at 640 channels); SD_AMD_FUSED_XATTN=0 / 1 forces it off / on
+_FUSED_ENV = os.environ.get("SD_AMD_FUSED_XATTN")
+FUSED_CROSS_ATTENTION = _FUSED_ENV != "0"
+FUSED_XATTN_MIN_ROWS = 0 if _FUSED_ENV == "1" else 131072
+
+
+def _use_fused_xattn(channels, head_dim, nk, n_img, batch):
+    if not FUSED_CROSS_ATTENTION or n_img % 64:
+        return False
+    if _FUSED_ENV != "1" and (channels != 320 or batch * n_img < FUSED_XATTN_MIN_ROWS):
+        return False
+    return ops.cross_attention_block_supported(channels, head_dim, nk, n_img)
 
 
 class CrossAttention(nn.Module):
@@ -85,8 +103,15 @@ class CrossAttention(nn.Module):
                 k, v, nk = kvx[:, :inner], kvx[:, inner:], N
         else:
             # cross-attention on the cached context K|V: to_q, the attention core and to_out are
-            # the per-step block the bench reports (``cross_attention_block``)
+            # the per-step block the bench reports (``cross_attention_block``); one fused kernel
+            # where the shape is supported, else the three launches
             ops.PROFILER.region = "cross_attention"
+            if t.stride(-1) == 1 and _use_fused_xattn(inner, self.dim_head, Lc, N, B):
+                out = ops.cross_attention_block(t, kv, self._pc_q, self._pc_o, batch=B, n_img=N, nk=Lc,
+                                                heads=self.heads, head_dim=self.dim_head, scale=self.scale,
+                                                residual=residual)
+                ops.PROFILER.region = None
+                return out
             q = ops.linear(self._pc_q, t)
             k, v, nk = kv[:, :inner], kv[:, inner:], Lc
         o = ops.attention(q, k, v, batch=B, heads=self.heads, nq=N, nk=nk, head_dim=self.dim_head, scale=self.scale)

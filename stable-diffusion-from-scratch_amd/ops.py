@@ -15,7 +15,7 @@ import math
 import torch
 
 from . import _lib
-from ._lib import (ACT_NONE, ACT_QUICK_GELU, AttentionArgs, ConvArgs, ConvPlanInfo, DdimArgs, GroupNormArgs,
+from ._lib import (ACT_NONE, ACT_QUICK_GELU, AttentionArgs, XAttnArgs, ConvArgs, ConvPlanInfo, DdimArgs, GroupNormArgs,
                    OUT_GEGLU_F16, OUT_NCHW_F32, OUT_NHWC_F16, OUT_ROWS_F32, check, lib)
 
 BK = 64          # K tile of the conv kernel (packed weight column padding)
@@ -505,6 +505,41 @@ def attention(q, k, v, *, batch, heads, nq, nk, head_dim, scale, out=None, causa
     if PROFILER.active:
         PROFILER.begin("attention", (batch, heads, nq, nk, head_dim))
     check(lib().sdk_attention(C.byref(a), _stream()), "attention")
+    if PROFILER.active:
+        PROFILER.end()
+    return out
+
+
+def cross_attention_block_supported(channels, head_dim, nk, n_img):
+    return bool(lib().sdk_cross_attention_block_supported(channels, head_dim, nk, n_img))
+
+
+def cross_attention_block(t, kv, pc_q: PackedConv, pc_o: PackedConv, *, batch, n_img, nk, heads, head_dim, scale,
+                          residual=None, out=None):
+    """One-kernel cross-attention block on a cached context K|V: ``to_out(attn(to_q(t), K, V)) + residual``.
+    t / residual: [batch*n_img, C] fp16; kv: [batch*nk, >= 2C] fp16 (K | V)."""
+    Cc = heads * head_dim
+    for x, n in ((t, "t"), (kv, "kv")):
+        _need_cuda(x, "cross_attention_block " + n)
+    if pc_q.k_total != Cc or pc_o.k_total != Cc or pc_q.N != Cc or pc_o.N != Cc:
+        raise ValueError("sd_amd.cross_attention_block: to_q / to_out must be channels x channels")
+    if out is None:
+        out = torch.empty(batch * n_img, Cc, dtype=torch.float16, device=t.device)
+    a = XAttnArgs()
+    a.t, a.kv, a.wq, a.wo = t.data_ptr(), kv.data_ptr(), pc_q.weight.data_ptr(), pc_o.weight.data_ptr()
+    a.bias = pc_o.bias.data_ptr() if pc_o.bias is not None else None
+    a.res = residual.data_ptr() if residual is not None else None
+    a.out = out.data_ptr()
+    a.t_ld, a.kv_ld, a.w_ld = t.stride(0), kv.stride(0), Cc
+    a.res_ld = residual.stride(0) if residual is not None else 0
+    a.out_ld = out.stride(0)
+    a.batch, a.n_img, a.nk, a.channels, a.head_dim, a.scale = batch, n_img, nk, Cc, head_dim, scale
+    if PROFILER.active:
+        # FLOPs of the three products it replaces (2 projections + attention core)
+        PROFILER.begin("cross_attention_block", None)
+        PROFILER._cur = PROFILER._cur[:2] + (4.0 * batch * n_img * Cc * Cc + 4.0 * batch * n_img * nk * Cc,) + \
+            PROFILER._cur[3:]
+    check(lib().sdk_cross_attention_block(C.byref(a), _stream()), "cross_attention_block")
     if PROFILER.active:
         PROFILER.end()
     return out

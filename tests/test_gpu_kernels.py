@@ -320,3 +320,41 @@ def test_group_norm_apply_concat(ops, silu):
         ref = F.silu(ref)
     assert y.shape == (B, H, W, C1 + C2)
     assert rel_l2(y, ref.permute(0, 2, 3, 1)) < 1e-3
+
+
+@pytest.mark.parametrize("B,N,C,D,nk", [(2, 4096, 320, 40, 77), (2, 1024, 640, 80, 77), (1, 256, 320, 64, 77),
+                                        (2, 64, 640, 64, 80), (3, 192, 320, 40, 13)])
+def test_cross_attention_block(ops, B, N, C, D, nk):
+    """Fused to_q + attention over the cached context K|V + to_out + residual (xattn.hip) against a
+    plain fp32 torch restatement (fp16 rounding of q / o / the projection output, as the separate
+    launches store them) and against the three-launch path."""
+    g = torch.Generator(device="cpu").manual_seed(N + C + nk)
+    H = C // D
+    t = torch.randn(B * N, C, generator=g).half().to(DEV)
+    kv = torch.randn(B * nk, 2 * C, generator=g).half().to(DEV)
+    res = torch.randn(B * N, C, generator=g).half().to(DEV)
+    wq = torch.randn(C, C, generator=g) / math.sqrt(C)
+    wo = torch.randn(C, C, generator=g) / math.sqrt(C)
+    bo = torch.randn(C, generator=g) * 0.1
+    pcq = ops.PackedConv([(wq, C)], None, device=DEV)
+    pco = ops.PackedConv([(wo, C)], bo, device=DEV)
+    assert ops.cross_attention_block_supported(C, D, nk, N)
+    y = ops.cross_attention_block(t, kv, pcq, pco, batch=B, n_img=N, nk=nk, heads=H, head_dim=D, scale=D ** -0.5,
+                                  residual=res)
+    q = (t.float() @ wq.half().float().to(DEV).T).half().float().view(B, N, H, D)
+    k = kv[:, :C].float().view(B, nk, H, D)
+    v = kv[:, C:].float().view(B, nk, H, D)
+    att = torch.softmax(torch.einsum("bnhd,bkhd->bhnk", q, k) * D ** -0.5, dim=-1)
+    o = torch.einsum("bhnk,bkhd->bnhd", att, v).reshape(B * N, C).half().float()
+    ref = (o @ wo.half().float().to(DEV).T + bo.to(DEV)).half().float() + res.float()
+    assert rel_l2(y, ref) < 3e-3
+    q3 = ops.linear(pcq, t)
+    o3 = ops.attention(q3, kv[:, :C], kv[:, C:], batch=B, heads=H, nq=N, nk=nk, head_dim=D, scale=D ** -0.5)
+    y3 = ops.linear(pco, o3, residual=res)
+    assert rel_l2(y, y3) < 3e-3
+
+
+def test_cross_attention_block_rejects_unsupported(ops):
+    assert not ops.cross_attention_block_supported(1280, 160, 77, 256)
+    assert not ops.cross_attention_block_supported(320, 40, 81, 4096)
+    assert not ops.cross_attention_block_supported(320, 40, 77, 100)

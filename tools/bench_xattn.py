@@ -1,0 +1,55 @@
+"""Fused cross-attention block (xattn.hip) vs the three launches it replaces (to_q GEMM,
+attention core, to_out GEMM + residual) on the SD-1 / SD-2 shapes at B=16, device time from HIP
+events over back-to-back launches."""
+import math
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+SHAPES = [("sd1_64x64", 16, 4096, 320, 40), ("sd1_32x32", 16, 1024, 640, 80), ("sd2_64x64", 16, 4096, 320, 64),
+          ("sd2_32x32", 16, 1024, 640, 64), ("sd1_64x64_cfg", 32, 4096, 320, 40)]
+
+
+def timeit(f, reps=20):
+    f()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        f()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e3
+
+
+def main():
+    import sd_amd_loader
+    sd_amd_loader.load()
+    from sd_amd import ops
+    nk = 77
+    for name, B, N, C, D in SHAPES:
+        H = C // D
+        t = torch.randn(B * N, C, device="cuda").half()
+        kv = torch.randn(B * nk, 2 * C, device="cuda").half()
+        res = torch.randn(B * N, C, device="cuda").half()
+        pcq = ops.PackedConv([(torch.randn(C, C) / math.sqrt(C), C)], None, device="cuda")
+        pco = ops.PackedConv([(torch.randn(C, C) / math.sqrt(C), C)], torch.zeros(C), device="cuda")
+        fused = lambda: ops.cross_attention_block(t, kv, pcq, pco, batch=B, n_img=N, nk=nk, heads=H, head_dim=D,
+                                                  scale=D ** -0.5, residual=res)
+
+        def three():
+            q = ops.linear(pcq, t)
+            o = ops.attention(q, kv[:, :C], kv[:, C:], batch=B, heads=H, nq=N, nk=nk, head_dim=D, scale=D ** -0.5)
+            return ops.linear(pco, o, residual=res)
+        tf, t3 = timeit(fused), timeit(three)
+        flops = 4.0 * B * N * C * C + 4.0 * B * N * nk * C
+        hbm = 3 * B * N * C * 2            # t + residual read, out written
+        print(f"{name:16s} B={B:3d} N={N:5d} C={C:4d} d={D:3d}  fused {tf:8.1f} us ({flops / tf / 1e6:7.1f} TFLOP/s, "
+              f"{hbm / tf / 1e6:6.2f} TB/s)   three launches {t3:8.1f} us   speedup {t3 / tf:5.2f}x", flush=True)
+
+
+if __name__ == "__main__":
+    main()
