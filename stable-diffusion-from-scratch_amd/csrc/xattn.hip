@@ -110,10 +110,30 @@ __global__ void __launch_bounds__(256, 1) xattn_block_kernel(XAttnParams p) {
   for (int e = tid; e < XKP * X::KLD + X::DP * X::VLD; e += 256) kl[e] = (half_t)0.f;
   for (int e = tid; e < XQ * 8; e += 256) qo[(e >> 3) * X::QLD + C + (e & 7)] = (half_t)0.f;
 
-  // ---- phase A: q = t Wq^T -> LDS (fp16, as the separate to_q GEMM stores it)
+  // ---- phase A: q = t Wq^T -> LDS (fp16, as the separate to_q GEMM stores it).  The t tile is
+  // staged into the q buffer first with every 16-B load in flight at once (one HBM latency
+  // instead of one per K-step); q overwrites it after all waves are past their MFMAs.
+  {
+    constexpr int C8 = C / 8;
+    constexpr int TL = XQ * C8 / 256;           // 16-B chunks per thread
+    static_assert(XQ * C8 % 256 == 0, "t tile chunks");
+    h8 tv[TL];
+#pragma unroll
+    for (int u = 0; u < TL; ++u) {
+      const int e = tid + 256 * u, row = e / C8, c8 = e - row * C8;
+      tv[u] = *reinterpret_cast<const h8*>(p.t + (size_t)(m0 + row) * p.t_ld + 8 * c8);
+    }
+#pragma unroll
+    for (int u = 0; u < TL; ++u) {
+      const int e = tid + 256 * u, row = e / C8, c8 = e - row * C8;
+      *reinterpret_cast<h8*>(qo + row * X::QLD + 8 * c8) = tv[u];
+    }
+  }
+  __syncthreads();
   {
     f4 acc[X::NB][4];
-    proj_wave<C, X::NB>(p.t + (size_t)m0 * p.t_ld, p.t_ld, p.wq, n_w, acc);
+    proj_wave<C, X::NB>(qo, X::QLD, p.wq, n_w, acc);
+    __syncthreads();   // every wave is done reading t
 #pragma unroll
     for (int j = 0; j < X::NB; ++j)
 #pragma unroll

@@ -45,11 +45,12 @@ def _ln_prep(ln: nn.LayerNorm, dev):
 
 # fused to_q + attention + to_out kernel for cross-attention on the cached context (xattn.hip),
 # routed where it measured faster than the three launches (tools/bench_xattn.py, MI355X: 320
-# channels at >= 131072 query rows, e.g. the classifier-free-guidance batch of 2 x 16 at 64x64:
-# 1.11x; level at 65536 rows, slower at 640 channels); SD_AMD_FUSED_XATTN=0 / 1 forces it off / on
+# channels at >= 65536 query rows — the 64x64 level at B=16: 1.07-1.11x, its CFG batch of 2 x 16:
+# 1.21x; slower at 640 channels, where one workgroup per CU is resident); SD_AMD_FUSED_XATTN=0 / 1
+# forces it off / on
 _FUSED_ENV = os.environ.get("SD_AMD_FUSED_XATTN")
 FUSED_CROSS_ATTENTION = _FUSED_ENV != "0"
-FUSED_XATTN_MIN_ROWS = 0 if _FUSED_ENV == "1" else 131072
+FUSED_XATTN_MIN_ROWS = 0 if _FUSED_ENV == "1" else 65536
 
 
 def _use_fused_xattn(channels, head_dim, nk, n_img, batch):

@@ -408,7 +408,7 @@ def test_tiny_ddim_cfg_vs_reference(sdk):
 
 
 def test_sd1_cfg_unet_fused_cross_attention_path(sdk):
-    """The classifier-free-guidance batch (2 x B at 64x64, >= 131072 query rows) routes the
+    """The classifier-free-guidance batch (2 x 16 at 64x64) routes the 320-channel
     cross-attentions through the fused block kernel; the UNet output matches the three-launch
     path on the same weights and inputs."""
     import importlib
