@@ -33,7 +33,14 @@ struct XAttnParams {
   int n_img;            // query tokens per image (multiple of 64)
   int nk;               // context tokens (<= 80)
   float c;              // softmax scale * log2(e)
+  unsigned long long* stamps;   // diagnostics (tools/bench_xattn.py --phases): 6 clock stamps per group, or null
 };
+
+__device__ __forceinline__ void stamp(const XAttnParams& p, int i) {
+  if (p.stamps && threadIdx.x == 0) p.stamps[blockIdx.x * 8 + i] = wall_clock64();
+}
+
+unsigned long long* g_xattn_stamps = nullptr;
 
 typedef _Float16 h4v __attribute__((ext_vector_type(4)));
 
@@ -47,10 +54,15 @@ struct XCfg {
   static constexpr int DP = (D + 15) / 16 * 16;     // head dim padded to the 16-wide MFMA K / N
   static constexpr int CW = C / 4;                  // channels per wave in the projections
   static constexpr int NB = CW / 16;
+  static constexpr int WP = C <= 320 ? 3 : 4;      // W prefetch depth (K-steps): 320 keeps 2 waves / SIMD
   static constexpr int QLD = C + 8;                 // q / o row stride (halfs); 8 zero pad columns
   static constexpr int KLD = DP + 8;                // K rows [key][d]
   static constexpr int VLD = XKP + 8;               // V^T rows [d][key]
-  static constexpr int LDS_HALFS = XQ * QLD + XKP * KLD + DP * VLD;
+  static constexpr int KVH = XKP * KLD + DP * VLD;  // one head's K + V^T (halfs)
+  // heads per iteration: 2 where the second K / V^T buffer keeps the resident group count
+  static constexpr int ONE = (XQ * QLD + KVH) * 2, TWO = (XQ * QLD + 2 * KVH) * 2;
+  static constexpr int HPI = (TWO <= 80 * 1024 || ONE > 80 * 1024) && H > 1 ? 2 : 1;
+  static constexpr int LDS_HALFS = XQ * QLD + HPI * KVH;
   static constexpr int LDS_BYTES = LDS_HALFS * 2;
   static_assert(C % 64 == 0 && CW % 16 == 0 && D % 8 == 0 && C % D == 0, "shape");
   static_assert(DP - D <= 8, "q padding columns cover the last head's d padding");
@@ -58,10 +70,11 @@ struct XCfg {
 };
 
 // D^T[n, m] = sum_k W[n, k] X[m, k] for the wave's NB 16-channel blocks x 4 16-pixel blocks.
-// X rows come from global (phase A: t) or LDS (phase C: o), W rows from global (L2-resident).
-// K-steps of 32, fully unrolled, fragments loaded two steps ahead (three register sets): the
-// W / t fragments come from L2 / HBM, and one step of prefetch leaves the MFMAs waiting.
-template <int C, int NB>
+// X rows come from LDS (t in phase A, o in phase C), W rows from global (L2-resident, shared by
+// every workgroup).  K-steps of 32, fully unrolled.  The W fragments are the long-latency operand:
+// they run WP K-steps ahead through a ring of WP + 1 register sets (the phase was L2-latency-bound
+// at two steps ahead: 13 us for 1.3 us of MFMAs); the LDS fragments run one step ahead.
+template <int C, int NB, int WP>
 __device__ __forceinline__ void proj_wave(const half_t* __restrict__ x, int x_ld, const half_t* __restrict__ w,
                                           int n_w, f4 (&acc)[NB][4]) {
   const int lane = threadIdx.x & 63, r16 = lane & 15, c16 = lane >> 4;
@@ -72,24 +85,32 @@ __device__ __forceinline__ void proj_wave(const half_t* __restrict__ x, int x_ld
   const half_t* wp = w + (size_t)(n_w + r16) * C + 8 * c16;
   const half_t* xp = x + (size_t)r16 * x_ld + 8 * c16;
   constexpr int KS = C / 32;
-  h8 fw[3][NB], fx[3][4];
-  auto load = [&](int ks, int slot) {
+  constexpr int WR = WP + 1;
+  h8 fw[WR][NB], fx[2][4];
+  auto load_w = [&](int ks) {
 #pragma unroll
-    for (int j = 0; j < NB; ++j) fw[slot][j] = *reinterpret_cast<const h8*>(wp + (size_t)j * 16 * C + 32 * ks);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) fx[slot][i] = *reinterpret_cast<const h8*>(xp + (size_t)i * 16 * x_ld + 32 * ks);
+    for (int j = 0; j < NB; ++j) fw[ks % WR][j] = *reinterpret_cast<const h8*>(wp + (size_t)j * 16 * C + 32 * ks);
   };
-  load(0, 0);
-  if (KS > 1) load(1, 1);
+  auto load_x = [&](int ks) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fx[ks & 1][i] = *reinterpret_cast<const h8*>(xp + (size_t)i * 16 * x_ld + 32 * ks);
+  };
+#pragma unroll
+  for (int ks = 0; ks < WP && ks < KS; ++ks) load_w(ks);
+  load_x(0);
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
-    if (ks + 2 < KS) load(ks + 2, (ks + 2) % 3);
-    const int sl = ks % 3;
+    if (ks + WP < KS) load_w(ks + WP);
+    if (ks + 1 < KS) load_x(ks + 1);
+    // keep the prefetch where it is: left alone, the scheduler sinks each load next to its
+    // MFMA (one step ahead, vmcnt(1) waits) to save registers
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int j = 0; j < NB; ++j)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[sl][j], fx[sl][i], acc[j][i], 0, 0, 0);
+        acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[ks % WR][j], fx[ks & 1][i], acc[j][i], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
@@ -98,8 +119,7 @@ __global__ void __launch_bounds__(256, 1) xattn_block_kernel(XAttnParams p) {
   using X = XCfg<C, D>;
   extern __shared__ __attribute__((aligned(16))) half_t xl[];
   half_t* qo = xl;                              // [64][QLD]
-  half_t* kl = qo + XQ * X::QLD;                // [80][KLD]
-  half_t* vt = kl + XKP * X::KLD;               // [DP][VLD]
+  half_t* kvl = qo + XQ * X::QLD;               // HPI x { K [80][KLD], V^T [DP][VLD] }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r16 = lane & 15, c16 = lane >> 4;
   const int m0 = blockIdx.x * XQ;
@@ -107,9 +127,10 @@ __global__ void __launch_bounds__(256, 1) xattn_block_kernel(XAttnParams p) {
   const int n_w = wave * X::CW;
 
   // zero: K / V^T padding (keys >= nk, d >= D) and the q pad columns
-  for (int e = tid; e < XKP * X::KLD + X::DP * X::VLD; e += 256) kl[e] = (half_t)0.f;
+  for (int e = tid; e < X::HPI * X::KVH; e += 256) kvl[e] = (half_t)0.f;
   for (int e = tid; e < XQ * 8; e += 256) qo[(e >> 3) * X::QLD + C + (e & 7)] = (half_t)0.f;
 
+  stamp(p, 0);
   // ---- phase A: q = t Wq^T -> LDS (fp16, as the separate to_q GEMM stores it).  The t tile is
   // staged into the q buffer first with every 16-B load in flight at once (one HBM latency
   // instead of one per K-step); q overwrites it after all waves are past their MFMAs.
@@ -130,9 +151,10 @@ __global__ void __launch_bounds__(256, 1) xattn_block_kernel(XAttnParams p) {
     }
   }
   __syncthreads();
+  stamp(p, 1);
   {
     f4 acc[X::NB][4];
-    proj_wave<C, X::NB>(qo, X::QLD, p.wq, n_w, acc);
+    proj_wave<C, X::NB, X::WP>(qo, X::QLD, p.wq, n_w, acc);
     __syncthreads();   // every wave is done reading t
 #pragma unroll
     for (int j = 0; j < X::NB; ++j)
@@ -146,104 +168,154 @@ __global__ void __launch_bounds__(256, 1) xattn_block_kernel(XAttnParams p) {
   }
   __syncthreads();
 
-  // ---- phase B: per head, exact softmax over <= 80 keys; o_h overwrites q_h in LDS.  The
-  // next head's K / V chunks (16 B) are loaded into registers while the current head
-  // computes, and written to LDS after its closing barrier.
+  stamp(p, 2);
+  // ---- phase B: HPI heads per barrier pair (independent chains the scheduler interleaves),
+  // exact softmax over <= 80 keys; o_h overwrites q_h in LDS.  The K / V chunks (16 B) of later
+  // iterations' heads are loaded into registers KVA iterations ahead and written to LDS after
+  // the current iteration's closing barrier.
   const half_t* kvb = p.kv + (size_t)b * p.nk * p.kv_ld;
   const int qrow = 16 * wave + r16;             // this lane's query (S^T column)
+  constexpr int HPI = X::HPI;
   constexpr int CH = D / 8;                     // 16-B chunks per key row
-  constexpr int NCH = (XKP * CH + 255) / 256;   // chunks per thread
-  h8 rk[NCH], rv[NCH];
-  auto kv_load = [&](int h) {
+  constexpr int NCH = (XKP * CH + 255) / 256;   // chunks per thread per head
+  constexpr int NIT = (X::H + HPI - 1) / HPI;
+  constexpr int KVA = HPI == 2 ? 1 : 2;          // iterations of K / V prefetch (register budget)
+  h8 rk[KVA][HPI][NCH], rv[KVA][HPI][NCH];
+  auto kv_load = [&](int it, int sl) {
 #pragma unroll
-    for (int u = 0; u < NCH; ++u) {
-      const int e = tid + 256 * u;
-      const int key = e / CH, ch = e - key * CH;
-      if (key < p.nk) {
-        const half_t* src = kvb + (size_t)key * p.kv_ld + h * D + 8 * ch;
-        rk[u] = *reinterpret_cast<const h8*>(src);
-        rv[u] = *reinterpret_cast<const h8*>(src + C);
+    for (int g = 0; g < HPI; ++g) {
+      const int h = it * HPI + g;
+#pragma unroll
+      for (int u = 0; u < NCH; ++u) {
+        const int e = tid + 256 * u;
+        const int key = e / CH, ch = e - key * CH;
+        if (key < p.nk && h < X::H) {
+          const half_t* src = kvb + (size_t)key * p.kv_ld + h * D + 8 * ch;
+          rk[sl][g][u] = *reinterpret_cast<const h8*>(src);
+          rv[sl][g][u] = *reinterpret_cast<const h8*>(src + C);
+        }
       }
     }
   };
-  kv_load(0);
-  for (int h = 0; h < X::H; ++h) {
+  kv_load(0, 0);
+  if (KVA == 2 && NIT > 1) kv_load(1, 1 % KVA);
+#pragma unroll 2
+  for (int it = 0; it < NIT; ++it) {
+    const int sl = it % KVA;
 #pragma unroll
-    for (int u = 0; u < NCH; ++u) {
-      const int e = tid + 256 * u;
-      const int key = e / CH, ch = e - key * CH;
-      if (key < p.nk) {
-        *reinterpret_cast<h8*>(kl + key * X::KLD + 8 * ch) = rk[u];
+    for (int g = 0; g < HPI; ++g) {
+      half_t* kl = kvl + g * X::KVH;
+      half_t* vt = kl + XKP * X::KLD;
 #pragma unroll
-        for (int q = 0; q < 8; ++q) vt[(8 * ch + q) * X::VLD + key] = rv[u][q];
+      for (int u = 0; u < NCH; ++u) {
+        const int e = tid + 256 * u;
+        const int key = e / CH, ch = e - key * CH;
+        if (key < p.nk && it * HPI + g < X::H) {
+          *reinterpret_cast<h8*>(kl + key * X::KLD + 8 * ch) = rk[sl][g][u];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) vt[(8 * ch + q) * X::VLD + key] = rv[sl][g][u][q];
+        }
       }
     }
     __syncthreads();
-    if (h + 1 < X::H) kv_load(h + 1);
-    // S^T[key, q] for the 5 key blocks
-    f4 s[XKP / 16];
+    if (it + KVA < NIT) kv_load(it + KVA, sl);
+    __builtin_amdgcn_sched_barrier(0);
+    const int ng = X::H - it * HPI < HPI ? X::H - it * HPI : HPI;   // heads this iteration
+    // S^T[key, q] for the 5 key blocks of each head
+    f4 s[HPI][XKP / 16];
 #pragma unroll
-    for (int kb = 0; kb < XKP / 16; ++kb) s[kb] = f4{};
+    for (int g = 0; g < HPI; ++g)
 #pragma unroll
-    for (int dd = 0; dd < X::DP; dd += 16) {
-      const h4v fq = *reinterpret_cast<const h4v*>(qo + qrow * X::QLD + h * D + dd + 4 * c16);
+      for (int kb = 0; kb < XKP / 16; ++kb) s[g][kb] = f4{};
 #pragma unroll
-      for (int kb = 0; kb < XKP / 16; ++kb) {
-        const h4v fk = *reinterpret_cast<const h4v*>(kl + (16 * kb + r16) * X::KLD + dd + 4 * c16);
-        s[kb] = __builtin_amdgcn_mfma_f32_16x16x16f16(fk, fq, s[kb], 0, 0, 0);
+    for (int g = 0; g < HPI; ++g) {
+      if (g < ng) {
+        const int h = it * HPI + g;
+        const half_t* kl = kvl + g * X::KVH;
+#pragma unroll
+        for (int dd = 0; dd < X::DP; dd += 16) {
+          const h4v fq = *reinterpret_cast<const h4v*>(qo + qrow * X::QLD + h * D + dd + 4 * c16);
+#pragma unroll
+          for (int kb = 0; kb < XKP / 16; ++kb) {
+            const h4v fk = *reinterpret_cast<const h4v*>(kl + (16 * kb + r16) * X::KLD + dd + 4 * c16);
+            s[g][kb] = __builtin_amdgcn_mfma_f32_16x16x16f16(fk, fq, s[g][kb], 0, 0, 0);
+          }
+        }
       }
     }
     // lane holds keys 16kb + 4*c16 + r of query qrow
-    float mx = -INFINITY;
+    float mx[HPI], sum[HPI], inv[HPI];
+    h4v pf[HPI][XKP / 16];
 #pragma unroll
-    for (int kb = 0; kb < XKP / 16; ++kb)
+    for (int g = 0; g < HPI; ++g) {
+      mx[g] = -INFINITY;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = 16 * kb + 4 * c16 + r;
-        const float v = key < p.nk ? s[kb][r] * p.c : -INFINITY;
-        s[kb][r] = v;
-        mx = fmaxf(mx, v);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    float sum = 0.f;
-    h4v pf[XKP / 16];
+      for (int kb = 0; kb < XKP / 16; ++kb)
 #pragma unroll
-    for (int kb = 0; kb < XKP / 16; ++kb)
+        for (int r = 0; r < 4; ++r) {
+          const int key = 16 * kb + 4 * c16 + r;
+          const float v = key < p.nk ? s[g][kb][r] * p.c : -INFINITY;
+          s[g][kb][r] = v;
+          mx[g] = fmaxf(mx[g], v);
+        }
+    }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float e = __builtin_amdgcn_exp2f(s[kb][r] - mx);
-        sum += e;
-        pf[kb][r] = (half_t)e;
-      }
-    sum += __shfl_xor(sum, 16, 64);
-    sum += __shfl_xor(sum, 32, 64);
-    const float inv = 1.f / sum;
+    for (int g = 0; g < HPI; ++g) mx[g] = fmaxf(mx[g], __shfl_xor(mx[g], 16, 64));
+#pragma unroll
+    for (int g = 0; g < HPI; ++g) mx[g] = fmaxf(mx[g], __shfl_xor(mx[g], 32, 64));
+#pragma unroll
+    for (int g = 0; g < HPI; ++g) {
+      sum[g] = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < XKP / 16; ++kb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = __builtin_amdgcn_exp2f(s[g][kb][r] - mx[g]);
+          sum[g] += e;
+          pf[g][kb][r] = (half_t)e;
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < HPI; ++g) sum[g] += __shfl_xor(sum[g], 16, 64);
+#pragma unroll
+    for (int g = 0; g < HPI; ++g) {
+      sum[g] += __shfl_xor(sum[g], 32, 64);
+      inv[g] = 1.f / sum[g];
+    }
     // O^T[d, q] = sum_key V^T[d, key] P^T[key, q]
 #pragma unroll
-    for (int dd = 0; dd < X::DP; dd += 16) {
-      f4 o = f4{};
+    for (int g = 0; g < HPI; ++g) {
+      if (g < ng) {
+        const int h = it * HPI + g;
+        const half_t* vt = kvl + g * X::KVH + XKP * X::KLD;
 #pragma unroll
-      for (int kb = 0; kb < XKP / 16; ++kb) {
-        const h4v fv = *reinterpret_cast<const h4v*>(vt + (dd + r16) * X::VLD + 16 * kb + 4 * c16);
-        o = __builtin_amdgcn_mfma_f32_16x16x16f16(fv, pf[kb], o, 0, 0, 0);
-      }
-      const int d0 = dd + 4 * c16;              // lane holds d0..d0+3 of query qrow
-      if (d0 < D) {
-        h4v w;
+        for (int dd = 0; dd < X::DP; dd += 16) {
+          f4 o = f4{};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) w[r] = (half_t)(o[r] * inv);
-        *reinterpret_cast<h4v*>(qo + qrow * X::QLD + h * D + d0) = w;
+          for (int kb = 0; kb < XKP / 16; ++kb) {
+            const h4v fv = *reinterpret_cast<const h4v*>(vt + (dd + r16) * X::VLD + 16 * kb + 4 * c16);
+            o = __builtin_amdgcn_mfma_f32_16x16x16f16(fv, pf[g][kb], o, 0, 0, 0);
+          }
+          const int d0 = dd + 4 * c16;          // lane holds d0..d0+3 of query qrow
+          if (d0 < D) {
+            h4v w;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) w[r] = (half_t)(o[r] * inv[g]);
+            *reinterpret_cast<h4v*>(qo + qrow * X::QLD + h * D + d0) = w;
+          }
+        }
       }
     }
-    __syncthreads();   // o_h visible; K / V^T free for the next head
+    __syncthreads();   // o of these heads visible; K / V^T buffers free for the next iteration
   }
 
+  stamp(p, 3);
   // ---- phase C: out = o Wo^T + bo (fp16) + residual, staged through LDS for row stores
   {
     f4 acc[X::NB][4];
-    proj_wave<C, X::NB>(qo, X::QLD, p.wo, n_w, acc);
+    proj_wave<C, X::NB, X::WP>(qo, X::QLD, p.wo, n_w, acc);
     __syncthreads();   // every wave is done reading o
+    stamp(p, 4);
 #pragma unroll
     for (int j = 0; j < X::NB; ++j) {
       const int n = n_w + 16 * j + 4 * c16;
@@ -272,6 +344,7 @@ __global__ void __launch_bounds__(256, 1) xattn_block_kernel(XAttnParams p) {
       *reinterpret_cast<h8*>(p.out + m * p.out_ld + 8 * c8) = v;
     }
   }
+  stamp(p, 5);
 }
 
 template <int C, int D>
@@ -293,6 +366,10 @@ int launch_xattn(const XAttnParams& p, int m, hipStream_t s) {
 
 using namespace sdk;
 
+// diagnostics only (not in sdk_amd.h): per-workgroup phase clock stamps into a device buffer of
+// 8 * groups uint64 (wall_clock64, 100 MHz), for tools/bench_xattn.py --phases; null turns it off
+extern "C" void sdk_xattn_debug_stamps(unsigned long long* dev) { g_xattn_stamps = dev; }
+
 extern "C" int sdk_cross_attention_block_supported(int32_t channels, int32_t head_dim, int32_t nk, int32_t n_img) {
   const bool cd = (channels == 320 && (head_dim == 40 || head_dim == 64)) ||
                   (channels == 640 && (head_dim == 80 || head_dim == 64));
@@ -310,7 +387,7 @@ extern "C" int sdk_cross_attention_block(const sdk_xattn_args* a, sdk_stream_t s
   if (a->w_ld != a->channels) return fail(SDK_EINVAL, "cross_attention_block: weight rows must be channels long");
   XAttnParams p{(const half_t*)a->t, (const half_t*)a->kv, (const half_t*)a->wq, (const half_t*)a->wo, a->bias,
                 (const half_t*)a->res, (half_t*)a->out, a->t_ld, a->kv_ld, a->res_ld, a->out_ld, a->n_img, a->nk,
-                a->scale * 1.4426950408889634f};
+                a->scale * 1.4426950408889634f, g_xattn_stamps};
   const int m = a->batch * a->n_img;
   hipStream_t s = (hipStream_t)stream;
   if (a->channels == 320) return a->head_dim == 40 ? launch_xattn<320, 40>(p, m, s) : launch_xattn<320, 64>(p, m, s);

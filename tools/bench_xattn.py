@@ -51,5 +51,39 @@ def main():
               f"{hbm / tf / 1e6:6.2f} TB/s)   three launches {t3:8.1f} us   speedup {t3 / tf:5.2f}x", flush=True)
 
 
+def phases():
+    """Per-workgroup phase durations of the fused kernel (wall_clock64 stamps, 100 MHz)."""
+    import ctypes
+    import sd_amd_loader
+    sd_amd_loader.load()
+    from sd_amd import ops
+    from sd_amd._lib import lib
+    nk = 77
+    names = ["t stage", "q proj", "heads", "o proj", "store"]
+    for name, B, N, C, D in SHAPES:
+        H = C // D
+        t = torch.randn(B * N, C, device="cuda").half()
+        kv = torch.randn(B * nk, 2 * C, device="cuda").half()
+        res = torch.randn(B * N, C, device="cuda").half()
+        pcq = ops.PackedConv([(torch.randn(C, C) / math.sqrt(C), C)], None, device="cuda")
+        pco = ops.PackedConv([(torch.randn(C, C) / math.sqrt(C), C)], torch.zeros(C), device="cuda")
+        groups = B * N // 64
+        st = torch.zeros(groups * 8, dtype=torch.int64, device="cuda")
+        lib().sdk_xattn_debug_stamps(ctypes.c_void_p(st.data_ptr()))
+        ops.cross_attention_block(t, kv, pcq, pco, batch=B, n_img=N, nk=nk, heads=H, head_dim=D, scale=D ** -0.5,
+                                  residual=res)
+        torch.cuda.synchronize()
+        lib().sdk_xattn_debug_stamps(None)
+        s = st.view(groups, 8)[:, :6].double().cpu()
+        d = (s[:, 1:] - s[:, :-1]) * 10.0 / 1000.0            # us
+        life = (s[:, 5] - s[:, 0]) * 10.0 / 1000.0
+        span = (s[:, 5].max() - s[:, 0].min()) * 10.0 / 1000.0
+        print(f"{name:16s} groups={groups:5d} span {span:7.1f} us  group life {life.mean():6.1f} us  " +
+              "  ".join(f"{n} {v:5.1f}" for n, v in zip(names, d.mean(0).tolist())), flush=True)
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "--phases":
+        phases()
+    else:
+        main()
