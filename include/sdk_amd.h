@@ -156,7 +156,8 @@ int sdk_group_norm_apply_ex(const sdk_group_norm_args* a, int32_t silu, const fl
                             const void* residual, int32_t res_ld, void* y, int32_t ld_y, sdk_stream_t stream);
 
 /* ---------------------------------------------------------------- LayerNorm
- * y = (x - mean) * rstd * gamma + beta over the last dim, fp16 in/out, fp32 math.
+ * y = (x - mean) * rstd * gamma + beta over the last dim, fp16 in/out, fp32 math; gamma / beta fp32,
+ * 16-byte aligned; cols a multiple of 8, <= 2048.
  * Replaces nn.LayerNorm norm1/2/3 (openai_model/attention.py:216-218,251-253).
  */
 int sdk_layer_norm(const void* x, void* y, int32_t rows, int32_t cols, int32_t ld_x, int32_t ld_y,

@@ -274,56 +274,83 @@ __global__ void __launch_bounds__(256) gn_apply_ex_kernel(const half_t* s0, cons
   }
 }
 
-// LayerNorm: one wave per row, row cached in registers (cols <= 64*8*MAXV).
+// LayerNorm: one wave per row at a time, row cached in registers (cols <= 64*8*LN_MAXV).  Waves
+// walk rows grid-stride with the next row's loads in flight while the current one reduces, gamma /
+// beta live in registers for the whole walk, and mean and variance come out of ONE pair of shuffle
+// chains: sums of (x - x0) and (x - x0)^2 around a pivot x0 taken from the row itself, so the
+// E[d^2] - E[d]^2 form does not cancel (|mean - x0| is of the order of the row's spread).
 constexpr int LN_MAXV = 4;
+template <int MAXV>
 __global__ void __launch_bounds__(256) layer_norm_kernel(const half_t* x, half_t* y, int rows, int cols, int ldx,
                                                          int ldy, const float* gamma, const float* beta, float eps) {
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
+  const int nwaves = gridDim.x * 4;
   const int c8 = cols / 8;
-  const half_t* xr = x + (size_t)row * ldx;
-  h8 v[LN_MAXV];
-  float s = 0.f;
+  float g[MAXV][8], bt[MAXV][8];
 #pragma unroll
-  for (int i = 0; i < LN_MAXV; ++i) {
-    const int k = lane + 64 * i;
-    v[i] = h8{};
-    if (k < c8) {
-      v[i] = *reinterpret_cast<const h8*>(xr + k * 8);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) s += (float)v[i][j];
-    }
-  }
-  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-  const float mean = s / cols;
-  float q = 0.f;
-#pragma unroll
-  for (int i = 0; i < LN_MAXV; ++i) {
+  for (int i = 0; i < MAXV; ++i) {
     const int k = lane + 64 * i;
     if (k < c8) {
+      const f4* gp = reinterpret_cast<const f4*>(gamma + k * 8);
+      const f4* bp = reinterpret_cast<const f4*>(beta + k * 8);
+      const f4 g0 = gp[0], g1 = gp[1], b0 = bp[0], b1 = bp[1];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float d = (float)v[i][j] - mean;
-        q += d * d;
+      for (int j = 0; j < 4; ++j) {
+        g[i][j] = g0[j]; g[i][4 + j] = g1[j];
+        bt[i][j] = b0[j]; bt[i][4 + j] = b1[j];
       }
     }
   }
-  for (int off = 32; off > 0; off >>= 1) q += __shfl_xor(q, off, 64);
-  const float rstd = rsqrtf(q / cols + eps);
-  half_t* yr = y + (size_t)row * ldy;
+  auto load = [&](int r, h8 (&v)[MAXV]) {
+    const half_t* xr = x + (size_t)r * ldx;
 #pragma unroll
-  for (int i = 0; i < LN_MAXV; ++i) {
-    const int k = lane + 64 * i;
-    if (k < c8) {
-      h8 o;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int c = k * 8 + j;
-        o[j] = (half_t)(((float)v[i][j] - mean) * rstd * gamma[c] + beta[c]);
-      }
-      *reinterpret_cast<h8*>(yr + k * 8) = o;
+    for (int i = 0; i < MAXV; ++i) {
+      const int k = lane + 64 * i;
+      v[i] = (r < rows && k < c8) ? *reinterpret_cast<const h8*>(xr + k * 8) : h8{};
     }
+  };
+  int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  h8 v[MAXV];
+  load(row, v);
+  for (; row < rows; row += nwaves) {
+    h8 nv[MAXV];
+    load(row + nwaves, nv);
+    const float x0 = __shfl((float)v[0][0], 0, 64);
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int k = lane + 64 * i;
+      if (k < c8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = (float)v[i][j] - x0;
+          s1 += d;
+          s2 += d * d;
+        }
+      }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      s1 += __shfl_xor(s1, off, 64);
+      s2 += __shfl_xor(s2, off, 64);
+    }
+    const float inv_n = 1.f / cols;
+    const float dm = s1 * inv_n;
+    const float var = fmaxf(s2 * inv_n - dm * dm, 0.f);
+    const float mean = x0 + dm;
+    const float rstd = rsqrtf(var + eps);
+    half_t* yr = y + (size_t)row * ldy;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int k = lane + 64 * i;
+      if (k < c8) {
+        h8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (half_t)(((float)v[i][j] - mean) * rstd * g[i][j] + bt[i][j]);
+        *reinterpret_cast<h8*>(yr + k * 8) = o;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) v[i] = nv[i];
   }
 }
 
@@ -416,8 +443,20 @@ extern "C" int sdk_layer_norm(const void* x, void* y, int32_t rows, int32_t cols
                               const float* gamma, const float* beta, float eps, sdk_stream_t stream) {
   if (!x || !y || !gamma || !beta) return fail(SDK_EINVAL, "layer_norm: null pointer");
   if (cols % 8 || ld_x % 8 || ld_y % 8 || cols > 64 * 8 * LN_MAXV) return fail(SDK_EINVAL, "layer_norm: cols");
+  if (((uintptr_t)gamma | (uintptr_t)beta) & 15) return fail(SDK_EINVAL, "layer_norm: gamma/beta 16-B alignment");
   if (rows <= 0) return SDK_OK;
-  hipLaunchKernelGGL(layer_norm_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream,
-                     (const half_t*)x, (half_t*)y, rows, cols, ld_x, ld_y, gamma, beta, eps);
+  // 4 rows (waves) per block; up to 8 resident blocks per CU on 256 CUs, each wave then walks rows
+  const int blocks = std::min((rows + 3) / 4, 2048);
+  hipStream_t s = (hipStream_t)stream;
+  const int c8 = cols / 8;
+  if (c8 <= 64)
+    hipLaunchKernelGGL(layer_norm_kernel<1>, dim3(blocks), dim3(256), 0, s, (const half_t*)x, (half_t*)y, rows, cols,
+                       ld_x, ld_y, gamma, beta, eps);
+  else if (c8 <= 128)
+    hipLaunchKernelGGL(layer_norm_kernel<2>, dim3(blocks), dim3(256), 0, s, (const half_t*)x, (half_t*)y, rows, cols,
+                       ld_x, ld_y, gamma, beta, eps);
+  else
+    hipLaunchKernelGGL(layer_norm_kernel<LN_MAXV>, dim3(blocks), dim3(256), 0, s, (const half_t*)x, (half_t*)y, rows,
+                       cols, ld_x, ld_y, gamma, beta, eps);
   return check_launch("layer_norm");
 }

@@ -185,6 +185,19 @@ def test_layer_norm(ops, C):
     assert rel_l2(y, ref) < 1e-3
 
 
+@pytest.mark.parametrize("M,C,offset", [(70001, 320, 0.0), (9000, 768, 30.0), (8193, 2048, -12.0), (5, 64, 100.0)])
+def test_layer_norm_rows_walk_and_offset_mean(ops, M, C, offset):
+    """More rows than resident waves (each wave walks rows with the next row prefetched), CLIP's
+    768, the 2048 maximum, and rows whose mean is far from 0 relative to their spread (the pivot
+    keeps the one-pass variance from cancelling)."""
+    g0 = torch.Generator().manual_seed(M + C)
+    x = (torch.randn(M, C, generator=g0) + offset).half()
+    g, b = torch.rand(C, generator=g0) + 0.5, torch.randn(C, generator=g0) * 0.1
+    y = ops.layer_norm(x.to(DEV), g.to(DEV), b.to(DEV), 1e-5)
+    ref = F.layer_norm(x.float(), (C,), g, b, 1e-5)
+    assert rel_l2(y, ref) < 1e-3
+
+
 @pytest.mark.parametrize("B,H,nq,nk,d", [
     (2, 8, 300, 300, 40), (1, 8, 256, 77, 80), (1, 8, 64, 64, 160), (2, 5, 200, 77, 64),
     (1, 2, 100, 100, 8), (1, 4, 130, 1024, 16), (1, 8, 4096, 4096, 40),
