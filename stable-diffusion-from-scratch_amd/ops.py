@@ -186,7 +186,7 @@ class _Autotune:
 
     Enabled by ``enable()`` (UNetModel/AutoEncoderKL.prepare(autotune=True)); the
     first call of each distinct problem times every candidate (HIP events, 3 reps
-    after a warm-up) and caches the fastest.  Never runs under graph capture."""
+    after a warm-up; SD_AMD_TUNE_REPS) and caches the fastest.  Never runs under graph capture."""
     VARIANTS = (2, 5, 7, 6, 4, 3, 8, 9, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26)
     SPLITS = (0, 1, 2, 4, 8)
 
@@ -197,6 +197,7 @@ class _Autotune:
         ev = os.environ.get("SD_AMD_TUNE_VARIANTS")       # candidate subset (benchmarking the tuner itself)
         if ev:
             self.VARIANTS = tuple(int(v) for v in ev.split(","))
+        self.reps = int(os.environ.get("SD_AMD_TUNE_REPS", "3"))   # timed launches per candidate
 
     def enable(self, on=True):
         self.enabled = on
@@ -252,7 +253,7 @@ class _Autotune:
                 check(lib().sdk_conv2d(C.byref(a), stream), "conv2d(autotune)")
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                for _ in range(3):
+                for _ in range(self.reps):
                     lib().sdk_conv2d(C.byref(a), stream)
                 e1.record()
                 e1.synchronize()
