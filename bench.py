@@ -25,6 +25,9 @@ import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+import sd_amd_loader  # noqa: E402  (registers the package as `sd_amd`; the HIP library loads on first use)
+
+sd_amd_loader.load()
 
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 PEAK_F16_TFLOPS = 2500.0        # MI355X dense fp16/bf16 MFMA (MI355X_MICROARCH.md, no sparsity)
@@ -35,14 +38,15 @@ SD1_UNET = dict(image_size=32, in_channels=4, out_channels=4, model_channels=320
                 transformer_depth=1, context_dim=768, use_checkpoint=False, legacy=False)
 SD_VAE = dict(double_z=True, z_channels=4, resolution=256, in_channels=3, out_ch=3, ch=128, ch_mult=[1, 2, 4, 4],
               num_res_blocks=2, attn_resolutions=[], dropout=0.0)
+UNCOND_OVERRIDE = dict(use_spatial_transformer=False, context_dim=None)
+SD2_OVERRIDE = dict(num_heads=-1, num_head_channels=64, context_dim=1024)
 CONFIGS = {
     "c3": dict(workload="sd1-txt2img-512-ddim50", unet=SD1_UNET, latent=64, ctx=(77, 768), batch=16),
-    "c2": dict(workload="ldm-uncond-256-ddim50", unet=dict(SD1_UNET, use_spatial_transformer=False,
-                                                           context_dim=None), latent=32, ctx=None, batch=8),
+    "c2": dict(workload="ldm-uncond-256-ddim50", unet=dict(SD1_UNET, **UNCOND_OVERRIDE), unet_override=UNCOND_OVERRIDE,
+               latent=32, ctx=None, batch=8),
     "c1": dict(workload="ddpm-pixel-32-10step", ddpm=True, image=32, batch=4, timesteps=10),
-    "c5": dict(workload="sd2shape-768-vpred-ddim50", unet=dict(SD1_UNET, num_heads=-1, num_head_channels=64,
-                                                               context_dim=1024), latent=96, ctx=(77, 1024),
-               batch=8, v=True),
+    "c5": dict(workload="sd2shape-768-vpred-ddim50", unet=dict(SD1_UNET, **SD2_OVERRIDE), unet_override=SD2_OVERRIDE,
+               latent=96, ctx=(77, 1024), batch=8, v=True),
 }
 
 
@@ -59,45 +63,91 @@ def synth_init_(module, seed, device):
             p.data = torch.ones(p.shape, device=device)
 
 
+def model_config(cfg):
+    """The LatentDiffusion config of a workload: the reference's Diffusion/config.yaml `model`
+    section (configs/sd-v1-txt2img.yaml, same targets/params) with the config's UNet overrides."""
+    import copy
+    import yaml
+    y = yaml.safe_load(open(os.path.join(ROOT, "configs", "sd-v1-txt2img.yaml")))["model"]
+    y = copy.deepcopy(y)
+    p = y["params"]
+    p["unet_config"]["params"].update(cfg.get("unet_override", {}))
+    if cfg["ctx"] is None:
+        p["cond_stage_config"] = "__is_unconditional__"       # conditioning_key -> None (C2)
+    elif cfg.get("v"):
+        p["parameterization"] = "v"                           # SD-2 shape (C5): synthetic 1024-wide context
+        p["cond_stage_config"] = None
+    return y
+
+
 def build_models(cfg, device, graph=False):
+    """LatentDiffusion built through the drop-in chain (instantiate_from_config on the reference's
+    YAML targets), seeded random weights materialised on the device.  Sampling calls
+    apply_model -> DiffusionWrapper.forward -> UNetModel (HIP graph replay when ``graph``)."""
     import sd_amd_loader
     sd_amd_loader.load()
-    from sd_amd.openai_model.model import UNetModel
-    from sd_amd.VAE.autoencoder import AutoEncoderKL
-    from sd_amd.DDIM.diffusion_modules import register_schedule
+    from sd_amd.Diffusion.utils import instantiate_from_config
     with torch.device("meta"):
-        unet = UNetModel(**cfg["unet"])
-        vae = AutoEncoderKL(ddconfig=SD_VAE, embed_dim=4)
-    unet = unet.to_empty(device=device)
-    vae = vae.to_empty(device=device)
+        ld = instantiate_from_config(model_config(cfg))
+    unet = ld.model.diffusion_model.to_empty(device=device)
+    vae = ld.first_stage_model.to_empty(device=device)
     synth_init_(unet, 1234, device)
     synth_init_(vae, 4321, device)
     unet.prepare(device)
     vae.prepare(device)
-    sch = register_schedule(1000, 0.00085, 0.012)
-    from sd_amd.graphs import GraphedUNet
-    graphed = GraphedUNet(unet)
+    ld.use_graphs(graph)
+    return unet, vae, ld
 
-    class LatentModel:
-        """LatentDiffusion.apply_model / decode_first_stage semantics (Diffusion/ddpm.py)."""
-        num_timesteps = 1000
-        alphas_cumprod = sch["alphas_cumprod"]
-        parameterization = "v" if cfg.get("v") else "eps"
-        scale_factor = 0.18215
 
-        def __init__(self):
-            self.device = device
-            self.graph = graph
+def make_one_step(sampler, ld, xT, ctx, ddim_steps, world, gathered):
+    """One bench step on one rank: 50-step DDIM over the rank's shard (x_T and context already in
+    HBM), the VAE decode, and — for N > 1 ranks — the one collective of the path, an all-gather of
+    the decoded images into ``gathered`` (rank-major, all_gather_into_tensor: RCCL over xGMI)."""
+    from sd_amd import distributed as sdd
+    B, shape = xT.shape[0], tuple(xT.shape[1:])
 
-        def apply_model(self, x, t, c):
-            if self.graph:
-                return graphed(x, t, c)
-            return unet(x, t, context=c)
+    def one_step():
+        z, _ = sampler.sample(S=ddim_steps, batch_size=B, shape=shape, conditioning=ctx, eta=0.0, x_T=xT,
+                              verbose=False, log_every_t=10 ** 9)
+        img = ld.decode_first_stage(z)
+        if world > 1:
+            sdd.gather(img.half(), world, out=gathered)
+        return img
+    return one_step
 
-        def decode_first_stage(self, z):
-            return vae.decode(z, pre_scale=1.0 / self.scale_factor)
 
-    return unet, vae, LatentModel()
+def timed_steps(one_step, steps, warmup, barrier, device):
+    """W untimed warm-up steps, then exactly K steps between barrier + synchronize pairs; the
+    elapsed time is the MAX over ranks."""
+    from sd_amd import distributed as sdd
+    img = None
+    for _ in range(warmup):
+        img = one_step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        img = one_step()
+    barrier()
+    return img, sdd.max_over_ranks(time.perf_counter() - t0, device=device)
+
+
+def make_barrier(dist, device):
+    def barrier():
+        if dist:
+            import torch.distributed as tdist
+            tdist.barrier()
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+    return barrier
+
+
+def rank_inputs(seed, world, rank, batch, latent_shape, ctx_shape, device):
+    """The rank's shard of the host-generated global batch (results independent of N)."""
+    from sd_amd import distributed as sdd
+    xT_all, ctx_all = sdd.global_inputs(seed, world, batch, latent_shape, ctx_shape)
+    xT = sdd.shard(xT_all, rank, world).to(device)
+    ctx = sdd.shard(ctx_all, rank, world).to(device) if ctx_all is not None else None
+    return xT, ctx
 
 
 def unet_gflops_per_image(cfg):
@@ -245,6 +295,59 @@ def pmc_traffic(args):
     return round(d["traffic_bytes_per_launch"])
 
 
+def _free_port():
+    import socket
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    return port
+
+
+def launch_ranks(n):
+    """``bench.py --gpus N`` (N > 1) started without a launcher: this GPU-free parent checks that N
+    devices are visible (device_count does not initialise the GPU on this image) and starts one
+    rank per GPU with torch.distributed.run as a CHILD process (no exec), exiting with its code."""
+    import subprocess
+    have = torch.cuda.device_count()
+    if have < n:
+        print(f"bench.py: --gpus {n} needs {n} visible GPUs, found {have}; refusing to report a "
+              f"{have}-GPU number as an {n}-GPU one", file=sys.stderr, flush=True)
+        sys.exit(3)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    sys.exit(subprocess.call(cmd, env=env))
+
+
+def setup_ranks(args):
+    """(world, rank, local, dist, device) — one process per GPU, checked against --gpus."""
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            launch_ranks(args.gpus)                  # does not return
+        world, rank, local = 1, 0, 0
+    else:
+        world = int(os.environ["WORLD_SIZE"])
+        rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: launched with WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr, flush=True)
+        sys.exit(3)
+    if torch.cuda.device_count() <= local:
+        print(f"bench.py: rank {rank} has no GPU of its own (local rank {local}, "
+              f"{torch.cuda.device_count()} visible)", file=sys.stderr, flush=True)
+        sys.exit(3)
+    dist = world > 1
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    if dist:
+        import torch.distributed as tdist
+        tdist.init_process_group("nccl", device_id=device)
+        assert tdist.get_world_size() == args.gpus
+    return world, rank, local, dist, device
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -263,16 +366,7 @@ def main():
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one HIP graph per UNet step")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = world > 1
-    if dist:
-        import torch.distributed as tdist
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    device = torch.device("cuda", local if dist else 0)
-    torch.cuda.set_device(device)
+    world, rank, local, dist, device = setup_ranks(args)
     cfg = CONFIGS[args.config]
     if cfg.get("ddpm"):
         main_ddpm(args, cfg, world, rank, local, dist, device)
@@ -283,59 +377,35 @@ def main():
     B = args.batch or cfg["batch"]
     L = cfg["latent"]
 
-    unet, vae, model = build_models(cfg, device, graph=not args.no_graph)
+    unet, vae, model = build_models(cfg, device, graph=False)
     from sd_amd.DDIM.ddim import DDIMSampler
     from sd_amd import ops
     sampler = DDIMSampler(model)
 
-    # host-generated global batch, sliced per rank (parity with any rank count)
-    from sd_amd import distributed as sdd
-    xT_all, ctx_all = sdd.global_inputs(2024, world, B, (4, L, L), cfg["ctx"])
-    xT = sdd.shard(xT_all, rank, world).to(device)
-    ctx = sdd.shard(ctx_all, rank, world).to(device) if ctx_all is not None else None
+    xT, ctx = rank_inputs(2024, world, rank, B, (4, L, L), cfg["ctx"], device)
     gathered = torch.empty(world * B, 3, 8 * L, 8 * L, dtype=torch.float16, device=device) if dist else None
+    one_step = make_one_step(sampler, model, xT, ctx, args.ddim_steps, world, gathered)
+    barrier = make_barrier(dist, device)
 
-    def one_step():
-        z, _ = sampler.sample(S=args.ddim_steps, batch_size=B, shape=(4, L, L), conditioning=ctx, eta=0.0, x_T=xT,
-                              verbose=False, log_every_t=10 ** 9)
-        img = model.decode_first_stage(z)
-        if dist:
-            sdd.gather(img.half(), world, out=gathered)
-        return img
-
-    def barrier():
-        if dist:
-            import torch.distributed as tdist
-            tdist.barrier()
-        torch.cuda.synchronize()
-
-    # the first warm-up step also autotunes every distinct conv problem (tile config x split-K);
-    # the UNet graph is captured on its first graphed call, after the eager autotuning call
+    # the first warm-up step (eager) also autotunes every distinct conv problem missing from the
+    # tuning table (tile config x split-K); the UNet graph is captured on the first graphed call
     cached = 0
     if args.tuning_cache and os.path.exists(args.tuning_cache) and not args.no_autotune:
         cached = ops.AUTOTUNE.load(args.tuning_cache)
     ops.AUTOTUNE.enable(not args.no_autotune)
-    model.graph = False
     one_step()
     ops.AUTOTUNE.enable(False)
     if args.tuning_out and rank == 0 and len(ops.AUTOTUNE.table) > cached:
         os.makedirs(os.path.dirname(os.path.abspath(args.tuning_out)), exist_ok=True)
         ops.AUTOTUNE.save(args.tuning_out)
-    model.graph = not args.no_graph
-    if model.graph:                      # capture the UNet graph (setup, not a sampling step)
+    model.use_graphs(not args.no_graph)
+    if not args.no_graph:                # capture the UNet graph (setup, not a sampling step)
         model.apply_model(xT, torch.full((B,), 999, dtype=torch.long, device=device), ctx)
-    for _ in range(max(args.warmup - 1, 0)):
-        one_step()
-    barrier()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        img = one_step()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    elapsed = sdd.max_over_ranks(elapsed, device=device)
+    img, elapsed = timed_steps(one_step, args.steps, max(args.warmup - 1, 0), barrier, device)
     finite = bool(torch.isfinite(img).all().item())
 
-    # UNet step latency at the config batch (HIP events around replays of the sampler's UNet call)
+    # UNet step latency at the config batch (HIP events around replays of the sampler's UNet call,
+    # through apply_model -> DiffusionWrapper -> graph replay)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     tts = torch.full((B,), 501, dtype=torch.long, device=device)
     model.apply_model(xT, tts, ctx)
@@ -351,14 +421,14 @@ def main():
     # per-kernel breakdown: one extra, untimed, eager step on rank 0 with HIP events
     # around every launch (not part of `value`)
     if not args.no_roofline and rank == 0:
-        model.graph = False
+        model.use_graphs(False)
         ops.PROFILER.start()
         z, _ = sampler.sample(S=args.ddim_steps, batch_size=B, shape=(4, L, L), conditioning=ctx, eta=0.0, x_T=xT,
                               verbose=False, log_every_t=10 ** 9)
         model.decode_first_stage(z)
         torch.cuda.synchronize()
         ops.PROFILER.stop()
-        model.graph = not args.no_graph
+        model.use_graphs(not args.no_graph)
 
     images = world * B * args.steps
     value = images / elapsed
@@ -368,7 +438,9 @@ def main():
            "N(0,1) latents, N(0,1) 77-token context)",
            "config": {"workload": cfg["workload"], "global_batch": world * B, "batch_per_gpu": B,
                       "latent": [4, L, L], "image": [3, 8 * L, 8 * L], "ddim_steps": args.ddim_steps, "eta": 0.0,
-                      "parallelism": f"dp{world}", "collective": "all_gather decoded images (RCCL)" if dist else None},
+                      "parallelism": f"dp{world}", "collective": "all_gather decoded images (RCCL)" if dist else None,
+                      "entry": "LatentDiffusion (configs/sd-v1-txt2img.yaml) -> DDIMSampler.sample -> "
+                               "decode_first_stage"},
            "unet_step_ms": round(unet_ms, 3), "finite": finite, "hip_graph": not args.no_graph,
            "autotuned_conv_problems": len(ops.AUTOTUNE.table), "tuning_cache_entries": cached}
     if not args.no_roofline and rank == 0:
@@ -406,11 +478,11 @@ def main():
             # which pairs it with a graph-replayed step of a rocprofv3 trace (device times)
             recs = ops.PROFILER.records
             ops.PROFILER.start()
-            model.graph = False
+            model.use_graphs(False)
             model.apply_model(xT, tts, ctx)
             torch.cuda.synchronize()
             ops.PROFILER.stop()
-            model.graph = not args.no_graph
+            model.use_graphs(not args.no_graph)
             seq = [[k, v, fl, list(sh) if isinstance(sh, tuple) else sh]
                    for k, v, fl, _, _, sh, _ in ops.PROFILER.records]
             ops.PROFILER.records = recs

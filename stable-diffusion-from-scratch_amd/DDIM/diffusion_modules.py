@@ -16,6 +16,11 @@ import torch
 
 
 def make_beta_schedule(schedule, n_timestep, linear_start=1e-4, linear_end=2e-2, cosine_s=8e-3):
+    with torch.device("cpu"):        # host constants, also inside a torch.device("meta") build
+        return _beta_schedule(schedule, n_timestep, linear_start, linear_end, cosine_s)
+
+
+def _beta_schedule(schedule, n_timestep, linear_start, linear_end, cosine_s):
     if schedule == "linear":
         betas = torch.linspace(linear_start ** 0.5, linear_end ** 0.5, n_timestep, dtype=torch.float64) ** 2
     elif schedule == "sqrt_linear":
@@ -39,7 +44,8 @@ def register_schedule(timesteps=1000, linear_start=1e-4, linear_end=2e-2, beta_s
         make_beta_schedule(beta_schedule, timesteps, linear_start, linear_end, cosine_s)
     alphas_cumprod = np.cumprod(1.0 - betas, axis=0)
     alphas_cumprod_prev = np.append(1.0, alphas_cumprod[:-1])
-    f = lambda a: torch.tensor(a, dtype=torch.float32)
+    # host constants: always CPU tensors, also when a model is built under torch.device("meta")
+    f = lambda a: torch.tensor(a, dtype=torch.float32, device="cpu")
     return {"betas": f(betas), "alphas_cumprod": f(alphas_cumprod), "alphas_cumprod_prev": f(alphas_cumprod_prev),
             "sqrt_alphas_cumprod": f(np.sqrt(alphas_cumprod)),
             "sqrt_one_minus_alphas_cumprod": f(np.sqrt(1.0 - alphas_cumprod)),

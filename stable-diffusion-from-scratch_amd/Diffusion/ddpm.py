@@ -5,8 +5,14 @@ conditioning wrapping (``ddpm.py:1139-1147,1269-1272`` → ``{'c_crossattn': [c]
 ``DiffusionWrapper.forward`` dispatch (``ddpm.py:46-73``), ``decode_first_stage``
 with the CompVis scaling ``z / scale_factor`` (``ldm/diffusion/ddpm.py:1095``;
 ``Diffusion/ddpm.py:728`` drops z — SURVEY Q8), ``parameterization``.
-Out of scope (training / Lightning / CLIP): losses, EMA, optimisers, data,
-logging, ``cond_stage_model`` — the conditioning tensor is passed in directly.
+``cond_stage_config`` is instantiated as the reference does (``ddpm.py:568-587``:
+``__is_first_stage__`` / ``__is_unconditional__`` / a target, frozen), so the reference YAML's
+``clip_encoder.modules.FrozenCLIPEmbedder`` resolves to the HIP-backed text tower;
+``get_learned_conditioning`` (``ddpm.py:1031-1051``) encodes through it.
+``use_graphs(True)`` makes ``DiffusionWrapper.forward`` replay one HIP graph per UNet call
+(``graphs.GraphedUNet``) — same chain apply_model → DiffusionWrapper.forward → UNetModel,
+one hipGraphLaunch per step instead of ~600 kernel launches.
+Out of scope (training / Lightning): losses, EMA, optimisers, data, logging.
 """
 from __future__ import annotations
 
@@ -25,19 +31,37 @@ class DiffusionWrapper(nn.Module):
         self.diffusion_model = instantiate_from_config(diff_model_config)
         self.conditioning_key = conditioning_key
         assert self.conditioning_key in [None, "concat", "crossattn", "hybrid", "adm"]
+        self._graphed = None
+        self._graphs_on = False
+
+    def use_graphs(self, on=True):
+        """Route the UNet call through one captured HIP graph per (shape, context) key (the
+        captured graphs are kept while switched off, e.g. for an eager profiling pass)."""
+        from ..graphs import GraphedUNet
+        if on and self._graphed is None:
+            self._graphed = GraphedUNet(self.diffusion_model)
+        self._graphs_on = bool(on)
+
+    def _unet(self, x, t, context=None):
+        if self._graphs_on:
+            if not torch.is_tensor(t):
+                t = torch.as_tensor(t, device=x.device)
+            return self._graphed(x, t.to(device=x.device, dtype=torch.long).reshape(-1).expand(x.shape[0]),
+                                 context)
+        return self.diffusion_model(x, t, context=context)
 
     def forward(self, x, t, c_concat: list = None, c_crossattn: list = None):
         if self.conditioning_key is None:
-            return self.diffusion_model(x, t)
+            return self._unet(x, t)
         if self.conditioning_key == "crossattn":
             cc = c_crossattn[0] if len(c_crossattn) == 1 else torch.cat(c_crossattn, 1)
-            return self.diffusion_model(x, t, context=cc)
+            return self._unet(x, t, context=cc)
         raise NotImplementedError(f"sd_amd: conditioning_key={self.conditioning_key} is not on the txt2img path")
 
 
 class LatentDiffusion(nn.Module):
     def __init__(self, first_stage_config, cond_stage_config=None, unet_config=None, num_timesteps_cond=None,
-                 cond_stage_key="image", cond_stage_trainable=False, concat_mode=True, cond_stage_forward=None,
+                 cond_stage_key="txt", cond_stage_trainable=False, concat_mode=True, cond_stage_forward=None,
                  conditioning_key=None, scale_factor=1.0, scale_by_std=False, timesteps=1000,
                  beta_schedule="linear", linear_start=1e-4, linear_end=2e-2, cosine_s=8e-3, given_betas=None,
                  parameterization="eps", image_size=256, channels=3, first_stage_key="image", log_every_t=100,
@@ -54,7 +78,10 @@ class LatentDiffusion(nn.Module):
         self.conditioning_key = conditioning_key
         self.model = DiffusionWrapper(unet_config, conditioning_key)
         self.first_stage_model = instantiate_from_config(first_stage_config)
-        self.cond_stage_model = None     # CLIP text encoder: outside the hot path (synthetic context)
+        self.cond_stage_trainable = cond_stage_trainable
+        self.cond_stage_key = cond_stage_key
+        self.cond_stage_forward = cond_stage_forward
+        self.instantiate_cond_stage(cond_stage_config)
         self.scale_factor = scale_factor
         self.image_size = image_size
         self.channels = channels
@@ -67,6 +94,37 @@ class LatentDiffusion(nn.Module):
     @property
     def device(self):
         return next(self.model.parameters()).device
+
+    def use_graphs(self, on=True):
+        self.model.use_graphs(on)
+
+    def instantiate_cond_stage(self, config):
+        """Reference ``Diffusion/ddpm.py:568-587`` (inference: the stage is always frozen)."""
+        if config is None or config == "__is_unconditional__":
+            self.cond_stage_model = None
+        elif config == "__is_first_stage__":
+            self.cond_stage_model = self.first_stage_model
+        else:
+            model = instantiate_from_config(config)
+            self.cond_stage_model = model.eval()
+            for param in self.cond_stage_model.parameters():
+                param.requires_grad = False
+
+    @torch.no_grad()
+    def get_learned_conditioning(self, c):
+        """Reference ``Diffusion/ddpm.py:1031-1051``: encode prompts (or token ids) with the cond stage."""
+        if self.cond_stage_forward is None:
+            if hasattr(self.cond_stage_model, "encode") and callable(self.cond_stage_model.encode):
+                c = self.cond_stage_model.encode(c)
+                from ..Distribution.distribution import DiagonalGaussianDistribution
+                if isinstance(c, DiagonalGaussianDistribution):
+                    c = c.mode()
+            else:
+                c = self.cond_stage_model(c)
+        else:
+            assert hasattr(self.cond_stage_model, self.cond_stage_forward)
+            c = getattr(self.cond_stage_model, self.cond_stage_forward)(c)
+        return c
 
     def apply_model(self, x_noisy, t, cond, return_ids=False):
         if isinstance(cond, dict):

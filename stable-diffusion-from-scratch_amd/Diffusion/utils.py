@@ -11,7 +11,8 @@ from __future__ import annotations
 import importlib
 
 _PKG = __name__.rsplit(".", 2)[0]      # "sd_amd"
-MIRRORED = ("openai_model", "Unet", "Encoder_Decoder", "VAE", "DDIM", "Diffusion", "DDPM")
+MIRRORED = ("openai_model", "Unet", "Encoder_Decoder", "VAE", "DDIM", "Diffusion", "DDPM", "clip_encoder",
+            "Distribution")
 
 
 def get_obj_from_str(string, reload=False):

@@ -24,15 +24,21 @@ def _needs(obj: str, deps) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    os.makedirs(BUILD, exist_ok=True)
+def build(force: bool = False, verbose: bool = False, diag: bool = False) -> str:
+    """``diag=True`` builds libsdk_amd_diag.so: the same ABI plus the conv kernel's diagnostic
+    ablations (variants 10-15, 27-30 — wrong outputs by design), for tools/ only (load it with
+    SD_AMD_LIB); the product library rejects those variant ids."""
+    bdir = BUILD + ("_diag" if diag else "")
+    lib = LIB.replace(".so", "_diag.so") if diag else LIB
+    os.makedirs(bdir, exist_ok=True)
     headers = [os.path.join(CSRC, "common.h"), os.path.join(HERE, "..", "include", "sdk_amd.h")]
     jobs = []
     for src in SOURCES:
         s = os.path.join(CSRC, src)
-        o = os.path.join(BUILD, src.replace(".hip", ".o"))
+        o = os.path.join(bdir, src.replace(".hip", ".o"))
         if force or _needs(o, [s] + headers):
-            jobs.append([HIPCC, *FLAGS, *EXTRA.get(src, []), "-c", s, "-o", o])
+            dflags = ["-DSDK_CONV_DIAGNOSTICS"] if diag else []
+            jobs.append([HIPCC, *FLAGS, *dflags, *EXTRA.get(src, []), "-c", s, "-o", o])
 
     def run(cmd):
         r = subprocess.run(cmd, capture_output=True, text=True)
@@ -44,11 +50,12 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
     with cf.ThreadPoolExecutor(max_workers=min(4, max(1, len(jobs)))) as ex:
         list(ex.map(run, jobs))
-    objs = [os.path.join(BUILD, s.replace(".hip", ".o")) for s in SOURCES]
-    if force or jobs or _needs(LIB, objs):
-        run([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o", LIB])
-    return LIB
+    objs = [os.path.join(bdir, s.replace(".hip", ".o")) for s in SOURCES]
+    if force or jobs or _needs(lib, objs):
+        run([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o", lib])
+    return lib
 
 
 if __name__ == "__main__":
-    print(build(verbose=True))
+    import sys
+    print(build(verbose=True, diag="--diag" in sys.argv))

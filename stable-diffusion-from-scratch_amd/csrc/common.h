@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <atomic>
 #include <string>
 
 #include "../../include/sdk_amd.h"
@@ -19,6 +21,20 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 void set_error(const std::string& msg);
 int fail(int code, const std::string& msg);
 int check_launch(const char* what);
+
+// Raise a kernel's dynamic-LDS cap on the CURRENT device.  hipFuncSetAttribute is per device, so
+// the "already done" state is one bit per device id (a process that drives a second GPU sets it
+// there too); `done` is a per-kernel-instantiation static.
+inline int ensure_dyn_lds(const void* fn, int bytes, std::atomic<unsigned long long>& done, const char* what) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return fail(SDK_EHIP, std::string(what) + ": hipGetDevice failed");
+  const unsigned long long bit = 1ull << (dev & 63);
+  if (done.load(std::memory_order_acquire) & bit) return SDK_OK;
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess)
+    return fail(SDK_EHIP, std::string(what) + ": cannot raise the dynamic LDS limit");
+  done.fetch_or(bit, std::memory_order_acq_rel);
+  return SDK_OK;
+}
 
 __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
 // erf by Abramowitz & Stegun 7.1.26 (|error| < 1.5e-7, far below the fp16 output's ulp):

@@ -1648,13 +1648,8 @@ using PhCfg10 = PhCfg<10, 8>;
 
 template <class PC, int DBG = 0, bool M16 = false>
 int launch_ph(const Params& p, hipStream_t s) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    if (hipFuncSetAttribute((const void*)conv_ph_kernel<PC, DBG, M16>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            PC::LDS_BYTES) != hipSuccess)
-      return fail(SDK_EHIP, "conv2d: cannot raise the dynamic LDS limit");
-    attr_set = true;
-  }
+  static std::atomic<unsigned long long> attr_set{0};
+  if (int e = ensure_dyn_lds((const void*)conv_ph_kernel<PC, DBG, M16>, PC::LDS_BYTES, attr_set, "conv2d")) return e;
   hipLaunchKernelGGL((conv_ph_kernel<PC, DBG, M16>), dim3(p.tiles_m * p.tiles_n, p.split), dim3(512),
                      PC::LDS_BYTES, s, p);
   return check_launch("conv_ph");
@@ -1709,17 +1704,24 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(Params p) {
 
 template <class CF>
 int launch_glds(const Params& p, hipStream_t s) {
-  static bool attr_set = false;   // raise the dynamic-LDS cap once per instantiation (not a per-call alloc)
-  if (!attr_set) {
-    if (hipFuncSetAttribute((const void*)conv_glds_kernel<CF>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            CF::LDS_BYTES) != hipSuccess)
-      return fail(SDK_EHIP, "conv2d: cannot raise the dynamic LDS limit");
-    attr_set = true;
-  }
+  static std::atomic<unsigned long long> attr_set{0};   // per device: the dynamic-LDS cap is raised once
+  if (int e = ensure_dyn_lds((const void*)conv_glds_kernel<CF>, CF::LDS_BYTES, attr_set, "conv2d")) return e;
   hipLaunchKernelGGL((conv_glds_kernel<CF>), dim3(p.tiles_m * p.tiles_n, p.split), dim3(CF::NT), CF::LDS_BYTES, s,
                      p);
   return check_launch("conv_glds");
 }
+
+#ifdef SDK_CONV_DIAGNOSTICS
+constexpr bool kDiagnostics = true;
+#else
+constexpr bool kDiagnostics = false;
+#endif
+inline bool is_diagnostic_variant(int v) { return (v >= 10 && v <= 15) || (v >= 27 && v <= 30); }
+// benchmark override of the tile configuration, read once when the library loads
+const int g_env_variant = [] {
+  const char* fe = getenv("SDK_CONV_VARIANT");
+  return fe ? atoi(fe) : -1;
+}();
 
 int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   if (!a) return fail(SDK_EINVAL, "conv2d: null args");
@@ -1837,12 +1839,17 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
     }
   }
   // forced configuration: the caller's autotuner (variant_hint = 1 + id) or, for
-  // benchmarks, SDK_CONV_VARIANT=id
-  const char* fe = getenv("SDK_CONV_VARIANT");
-  const int forced = a->variant_hint > 0 ? a->variant_hint - 1 : (fe ? atoi(fe) : -1);
+  // benchmarks, SDK_CONV_VARIANT=id (read once, at library load)
+  const int forced = a->variant_hint > 0 ? a->variant_hint - 1 : g_env_variant;
   // ids: 0 register-staged; 2..7 LDS-DMA configs; 8, 9 phased 256x256; 10..15 diagnostics;
   // 16..19 deep-ring LDS-DMA configs; 20, 21 phased 256x256 on v_mfma_f32_16x16x32_f16;
-  // 22..26 LDS-DMA configs 5, 7, 6, 19, 18 on v_mfma_f32_16x16x32_f16
+  // 22..26 LDS-DMA configs 5, 7, 6, 19, 18 on v_mfma_f32_16x16x32_f16; 27..30 diagnostics.
+  // The diagnostic ablations compute wrong outputs by design: the product library rejects them,
+  // only the separate diagnostics build (-DSDK_CONV_DIAGNOSTICS, libsdk_amd_diag.so) runs them.
+  if (is_diagnostic_variant(forced) && !kDiagnostics)
+    return fail(SDK_EINVAL, "conv2d: variant " + std::to_string(forced) +
+                                " is a diagnostic ablation (only in libsdk_amd_diag.so)");
+  if (forced > 30 || forced == 1) return fail(SDK_EINVAL, "conv2d: unknown variant " + std::to_string(forced));
   const int fbase = forced;
   const bool fvalid = forced >= 0 && forced != 1 && forced <= 30;
   const bool fgeglu = (fbase <= 4 || fbase >= 8) && fbase != 22 && fbase != 23 && fbase != 24;
@@ -1919,12 +1926,14 @@ extern "C" int sdk_conv2d(const sdk_conv_args* a, sdk_stream_t stream) {
     case 7: rc = launch_glds<Cfg128x320>(p, s); break;
     case 8: rc = launch_ph<PhCfg8>(p, s); break;
     case 9: rc = launch_ph<PhCfg10>(p, s); break;
+#ifdef SDK_CONV_DIAGNOSTICS
     case 10: rc = launch_ph<PhCfg8, 1>(p, s); break;   // diagnostics: no DMA
     case 11: rc = launch_ph<PhCfg8, 2>(p, s); break;   // diagnostics: no MFMA
     case 12: rc = launch_ph<PhCfg8, 4>(p, s); break;   // diagnostics: DMA from the zero page
     case 13: rc = launch_ph<PhCfg8, 64>(p, s); break;  // diagnostics: no epilogue stores
     case 14: rc = launch_ph<PhCfg8, 16>(p, s); break;  // diagnostics: W from the zero page
     case 15: rc = launch_ph<PhCfg8, 32>(p, s); break;  // diagnostics: A from the zero page
+#endif
     case 16: rc = launch_glds<Cfg128x128r4>(p, s); break;
     case 17: rc = launch_glds<Cfg256x128r3>(p, s); break;
     case 18: rc = launch_glds<Cfg128x128r3>(p, s); break;
@@ -1936,10 +1945,12 @@ extern "C" int sdk_conv2d(const sdk_conv_args* a, sdk_stream_t stream) {
     case 24: rc = launch_glds<Cfg256x160m>(p, s); break;
     case 25: rc = launch_glds<Cfg128x256r3m>(p, s); break;
     case 26: rc = launch_glds<Cfg128x128r3m>(p, s); break;
+#ifdef SDK_CONV_DIAGNOSTICS
     case 27: rc = launch_ph<PhCfg8, 128>(p, s); break;   // diagnostics: no W DMA issued
     case 28: rc = launch_ph<PhCfg8, 256>(p, s); break;   // diagnostics: no A DMA issued
     case 29: rc = launch_ph<PhCfg8, 512>(p, s); break;   // diagnostics: A DMAs read W rows (cheap addressing, L2)
     case 30: rc = launch_ph<PhCfg8, 1024>(p, s); break;  // diagnostics: A DMAs read the centre tap (no masks/halo)
+#endif
     default:
       hipLaunchKernelGGL(conv_igemm_kernel, grid, dim3(NT), 0, s, p);
       rc = check_launch("conv_igemm");

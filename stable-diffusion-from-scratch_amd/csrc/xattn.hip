@@ -350,13 +350,9 @@ __global__ void __launch_bounds__(256, 1) xattn_block_kernel(XAttnParams p) {
 template <int C, int D>
 int launch_xattn(const XAttnParams& p, int m, hipStream_t s) {
   using X = XCfg<C, D>;
-  static bool attr = false;
-  if (!attr) {
-    if (hipFuncSetAttribute((const void*)xattn_block_kernel<C, D>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            X::LDS_BYTES) != hipSuccess)
-      return fail(SDK_EHIP, "cross_attention_block: cannot raise the dynamic LDS limit");
-    attr = true;
-  }
+  static std::atomic<unsigned long long> attr{0};
+  if (int e = ensure_dyn_lds((const void*)xattn_block_kernel<C, D>, X::LDS_BYTES, attr, "cross_attention_block"))
+    return e;
   hipLaunchKernelGGL((xattn_block_kernel<C, D>), dim3(m / XQ), dim3(X::NT), X::LDS_BYTES, s, p);
   return check_launch("xattn_block");
 }

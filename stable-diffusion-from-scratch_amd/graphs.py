@@ -1,34 +1,62 @@
 """HIP-graph replay of the UNet forward (one sampler step's ~600 kernel launches).
 
 ``GraphedUNet(unet)(x, timesteps, context)`` captures ``unet.forward`` once per
-(input shape, context tensor) key with ``torch.cuda.graph`` and afterwards replays it:
-the inputs are copied into the graph's static buffers, the whole step is one
-``hipGraphLaunch``.  Everything the forward launches goes through the C ABI on the
-current stream, so it is captured like any torch op.  Preconditions (checked or
-documented): run one eager step first so the conv autotuner, the split-K / GroupNorm
-workspace and the context K/V cache are settled — the capture itself must not
-allocate workspace or time kernels; the returned tensor is the graph's static output
-and is overwritten by the next replay (the DDIM update consumes it immediately).
-The reference has no counterpart (eager PyTorch, ``ldm/models/diffusion/ddim.py``
-calls ``apply_model`` per step); this is the MI355X launch-overhead remedy."""
+(input shapes, context tensor) and afterwards replays it: the inputs are copied into
+the graph's static buffers, the whole step is one ``hipGraphLaunch``.  Everything the
+forward launches goes through the C ABI on the current stream, so it is captured like
+any torch op.
+
+Soundness rules (each one is what a replay reads from memory it does not own):
+* the graph key holds the context tensor ITSELF (identity + ``_version``), never its
+  address — a new conditioning that the caching allocator places at an old one's address
+  gets its own capture;
+* an entry keeps strong references to the context and to the cross-attention K/V it
+  was captured with, so model-side cache eviction cannot free memory a replay reads;
+* workspaces (split-K slabs, GroupNorm partials) are never freed while graphs may hold
+  their pointers (``ops._Workspace`` retires, never releases, a grown buffer);
+* re-packing the weights (``UNetModel.prepare`` after ``load_state_dict``) bumps the
+  model's ``prepare_generation`` and drops every graph.
+Preconditions: run one eager step first so the conv autotuner, the workspaces and the
+context K/V cache are settled; the returned tensor is the graph's static output and is
+overwritten by the next replay (the DDIM update consumes it immediately).
+The reference has no counterpart (eager PyTorch, ``ldm/diffusion/ddim.py`` calls
+``apply_model`` per step); this is the MI355X launch-overhead remedy."""
 from __future__ import annotations
+
+from collections import OrderedDict
 
 import torch
 
 
 class GraphedUNet:
+    MAX_GRAPHS = 8
+
     def __init__(self, unet):
         self.unet = unet
-        self.graphs = {}
+        self.graphs = OrderedDict()
+        self._gen = getattr(unet, "prepare_generation", None)
 
-    def _key(self, x, timesteps, context):
-        ctx = None if context is None else (context.data_ptr(), context._version, tuple(context.shape))
+    @staticmethod
+    def _key(x, timesteps, context):
+        ctx = None if context is None else (id(context), tuple(context.shape), context.dtype)
         return tuple(x.shape), x.dtype, tuple(timesteps.shape), ctx
+
+    def _valid(self, ent, context):
+        if context is None:
+            return ent["ctx"] is None
+        return ent["ctx"] is context and ent["ctx_version"] == context._version
 
     @torch.no_grad()
     def __call__(self, x, timesteps, context=None):
+        gen = getattr(self.unet, "prepare_generation", None)
+        if gen != self._gen:
+            self.reset()
+            self._gen = gen
         key = self._key(x, timesteps, context)
         ent = self.graphs.get(key)
+        if ent is not None and not self._valid(ent, context):
+            del self.graphs[key]
+            ent = None
         if ent is None:
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("GraphedUNet: nested capture")
@@ -38,15 +66,22 @@ class GraphedUNet:
             with torch.cuda.stream(side):          # settle caches/attributes outside the capture
                 self.unet(sx, st, context=context)
             torch.cuda.current_stream().wait_stream(side)
+            kv = None
+            if context is not None and hasattr(self.unet, "_context_kv"):
+                kv = self.unet._context_kv(context)[0]     # the K/V the capture will read (cache hit)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 out = self.unet(sx, st, context=context)
-            ent = self.graphs[key] = (g, sx, st, out)
-        g, sx, st, out = ent
-        sx.copy_(x)
-        st.copy_(timesteps)
-        g.replay()
-        return out
+            ent = {"graph": g, "x": sx, "t": st, "out": out, "ctx": context,
+                   "ctx_version": None if context is None else context._version, "kv": kv}
+            self.graphs[key] = ent
+            while len(self.graphs) > self.MAX_GRAPHS:
+                self.graphs.popitem(last=False)
+        self.graphs.move_to_end(key)
+        ent["x"].copy_(x)
+        ent["t"].copy_(timesteps)
+        ent["graph"].replay()
+        return ent["out"]
 
     def reset(self):
         self.graphs.clear()

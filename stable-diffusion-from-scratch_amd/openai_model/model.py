@@ -17,6 +17,8 @@ every conv/linear/norm/attention runs in libsdk_amd.so:
 """
 from __future__ import annotations
 
+from collections import OrderedDict
+
 import torch
 from torch import nn
 
@@ -296,13 +298,30 @@ class UNetModel(nn.Module):
         self._sts = [m for m in self.modules() if isinstance(m, SpatialTransformer)]
         self._prepared_on = dev
         self._ctx_cache = None
+        # packed weights were replaced: graphs captured on the old ones must be dropped
+        self.prepare_generation = getattr(self, "prepare_generation", 0) + 1
+
+    # contexts whose K/V stay resident (cond, uncond, their CFG concat, one spare)
+    CONTEXT_CACHE_SIZE = 4
 
     def _context_kv(self, context):
+        """K|V of every cross-attention for ``context``, computed once per conditioning tensor
+        (step-invariant across the sampler loop, reference ``ldm/diffusion/ddim.py:168-180``).
+
+        The cache is keyed on tensor IDENTITY: an entry holds a strong reference to its context
+        tensor (so neither its memory block nor its ``id`` can be handed to another tensor while
+        the entry lives) and the tensor's ``_version`` at projection time (an in-place write
+        misses).  A different conditioning therefore never hits another's K/V, whatever address
+        the caching allocator gives it.  LRU eviction drops only the oldest entry; a captured
+        HIP graph keeps its own reference to the K/V it reads (``graphs.GraphedUNet``)."""
         if context is None:
             return None, None
-        key = (context.data_ptr(), context._version, tuple(context.shape), context.dtype)
-        if self._ctx_cache is not None and key in self._ctx_cache:
-            return self._ctx_cache[key], context.shape[1]
+        if self._ctx_cache is None:
+            self._ctx_cache = OrderedDict()
+        ent = self._ctx_cache.get(id(context))
+        if ent is not None and ent[0] is context and ent[1] == context._version:
+            self._ctx_cache.move_to_end(id(context))
+            return ent[2], context.shape[1]
         B, L, D = context.shape
         if context.dtype == torch.float16:
             c2 = context.reshape(B * L, D).contiguous()
@@ -311,11 +330,14 @@ class UNetModel(nn.Module):
         kv = {}
         for st in self._sts:
             kv[id(st)] = st.context_kv(c2)
-        # a few contexts stay cached (the batch halves of a two-lane step, cond / uncond)
-        if self._ctx_cache is None or len(self._ctx_cache) >= 4:
-            self._ctx_cache = {}
-        self._ctx_cache[key] = kv
+        self._ctx_cache[id(context)] = (context, context._version, kv)
+        self._ctx_cache.move_to_end(id(context))
+        while len(self._ctx_cache) > self.CONTEXT_CACHE_SIZE:
+            self._ctx_cache.popitem(last=False)
         return kv, L
+
+    def clear_context_cache(self):
+        self._ctx_cache = None
 
     # ------------------------------------------------------------------ forward
     @torch.no_grad()
@@ -329,6 +351,11 @@ class UNetModel(nn.Module):
         t = timesteps
         if not torch.is_tensor(t):
             t = torch.tensor(t)
+        if t.is_floating_point():
+            # the reference embeds timesteps[:, None].float() (openai_model/utils.py:234-242); the
+            # embedding kernel takes integer steps, so a fractional step must not be truncated
+            if not bool((t == t.round()).all()):
+                raise ValueError("sd_amd.UNetModel: fractional timesteps are not supported (integer steps only)")
         t = t.to(device=x.device, dtype=torch.int64).reshape(-1)
         if t.numel() == 1 and B > 1:
             t = t.expand(B).contiguous()

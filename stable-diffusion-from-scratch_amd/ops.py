@@ -43,11 +43,20 @@ class _Workspace:
     """Growable scratch buffers (split-K slabs, GroupNorm partials), one per (device, lane).
     Calls of one lane are stream-ordered on one stream, so its buffer is safe to reuse;
     work issued concurrently on another stream must run under another lane
-    (``with WORKSPACE.use_lane(i)``)."""
+    (``with WORKSPACE.use_lane(i)``).
+
+    A grown buffer is RETIRED, not freed: a HIP graph captured earlier holds the old
+    pointer and writes through it on every replay, so its memory must stay owned by this
+    workspace for the process lifetime (the superseded sizes sum to less than the final one
+    when growth doubles; ``release_retired()`` is for callers that dropped every graph)."""
 
     def __init__(self):
         self.buf = {}
+        self.retired = []
         self.lane = 0
+
+    def release_retired(self):
+        self.retired.clear()
 
     def use_lane(self, lane: int):
         import contextlib
@@ -67,6 +76,9 @@ class _Workspace:
         if b is None or b.numel() < nbytes:
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("sd_amd: workspace must be sized before graph capture (run one warm-up step)")
+            if b is not None:
+                self.retired.append(b)
+                nbytes = max(nbytes, 2 * b.numel())       # geometric growth bounds the retired total
             b = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
             self.buf[key] = b
         return b
@@ -194,6 +206,7 @@ class _Autotune:
         import os
         self.enabled = False
         self.table = {}
+        self.timed = 0
         ev = os.environ.get("SD_AMD_TUNE_VARIANTS")       # candidate subset (benchmarking the tuner itself)
         if ev:
             self.VARIANTS = tuple(int(v) for v in ev.split(","))
@@ -262,10 +275,18 @@ class _Autotune:
                     best_t, best = t, (v + 1, info.split_k)
         a.variant_hint, a.split_k = 0, 0
         self.table[key] = best
+        self.timed += 1
+        if self.timed % 10 == 0:             # progress (a full re-tune takes minutes)
+            import sys
+            print(f"sd_amd autotune: {self.timed} conv problems timed", file=sys.stderr, flush=True)
         return best
 
 
 AUTOTUNE = _Autotune()
+
+
+# tests / benchmarks: force one tile configuration on every conv call (None = planner / autotuner)
+FORCE_VARIANT = None
 
 
 def conv2d(pc: PackedConv, x, *, ksize=None, stride=1, pad=None, pad_end=0, upsample=False, gn=None, silu=False,
@@ -319,6 +340,8 @@ def conv2d(pc: PackedConv, x, *, ksize=None, stride=1, pad=None, pad_end=0, upsa
     tuned = AUTOTUNE.choose(a, pc, dev) if (AUTOTUNE.enabled or AUTOTUNE.table) else None
     if tuned is not None:
         a.variant_hint, a.split_k = tuned
+    if variant is None:
+        variant = FORCE_VARIANT
     if variant is not None:
         a.variant_hint = variant + 1
     if split_k is not None:

@@ -1,0 +1,120 @@
+"""bench.py's data-parallel structure on the CPU (gloo, world_size 2) and its launcher checks.
+
+The per-rank step is bench's own code — ``rank_inputs`` (shard of the host-generated global
+batch), ``make_one_step`` (sample → decode → all-gather into the rank-major buffer) and
+``timed_steps`` (warm-up, barrier-bracketed timed steps, max over ranks) — with the GPU sampler
+and decoder replaced by CPU stand-ins built on the oracle's DDIM update.  ``sdd.gather`` is the
+same ``all_gather_into_tensor`` call the nccl (RCCL) branch makes, so the gathered layout is the
+one the 8-GPU run produces; it must equal the single-process result bit for bit.
+Reference basis: samples of a batch never interact (``ldm/diffusion/ddim.py:114-165``)."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+class _StubSampler:
+    """DDIMSampler.sample's signature; ε = a per-row function of (x, context) → shard-independent."""
+
+    def sample(self, S, batch_size, shape, conditioning=None, eta=0.0, x_T=None, verbose=False, log_every_t=100):
+        from oracle import schedule as osch
+        tab = osch.ddim_tables(S, 0.0)
+        x = x_T.float().clone()
+        assert x.shape == (batch_size,) + tuple(shape)
+        bias = conditioning.float().mean(dim=(1, 2)).view(-1, 1, 1, 1)
+        for i in range(S):
+            index = S - i - 1
+            eps = torch.tanh(x) * 0.5 + bias
+            xp, _ = osch.ddim_step(x.numpy(), eps.numpy(), osch.ddim_step_scalars(tab, index))
+            x = torch.from_numpy(xp)
+        return x, {}
+
+
+class _StubLD:
+    def decode_first_stage(self, z):
+        return torch.nn.functional.interpolate(z[:, :3], scale_factor=8, mode="nearest")
+
+
+def _worker(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import bench
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cpu")
+        B, L = 3, 8
+        xT, ctx = bench.rank_inputs(2024, world, rank, B, (4, L, L), (5, 16), dev)
+        assert xT.shape == (B, 4, L, L) and ctx.shape == (B, 5, 16)
+        gathered = torch.empty(world * B, 3, 8 * L, 8 * L, dtype=torch.float16)
+        one_step = bench.make_one_step(_StubSampler(), _StubLD(), xT, ctx, 4, world, gathered)
+        barrier = bench.make_barrier(True, dev)
+        img, elapsed = bench.timed_steps(one_step, 2, 1, barrier, dev)
+        assert img.shape == (B, 3, 8 * L, 8 * L) and elapsed > 0
+        from sd_amd import distributed as sdd
+        t = sdd.max_over_ranks(0.5 + rank)
+        if rank == 0:
+            out_q.put((gathered, t))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_dp_step_matches_single_process():
+    import sd_amd_loader
+    sd_amd_loader.load()
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    gathered, t = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import bench
+    xg, cg = bench.rank_inputs(2024, 1, 0, world * 3, (4, 8, 8), (5, 16), torch.device("cpu"))
+    z, _ = _StubSampler().sample(4, world * 3, (4, 8, 8), conditioning=cg, x_T=xg)
+    ref = _StubLD().decode_first_stage(z).half()
+    assert torch.equal(gathered, ref)
+    assert t == 1.5
+
+
+def _run_bench(args, env_extra=None):
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                          env=env, timeout=300, cwd=ROOT)
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    """--gpus N without a launcher spawns N ranks only if N GPUs are visible; otherwise it fails
+    fast, non-zero, and never prints a bench line (here: no GPU at all)."""
+    r = _run_bench(["--gpus", "2", "--steps", "1", "--warmup", "0"], {"HIP_VISIBLE_DEVICES": ""})
+    assert r.returncode != 0
+    assert "needs 2 visible GPUs" in r.stderr
+    assert '"metric"' not in r.stdout
+
+
+def test_bench_rejects_world_size_mismatch():
+    r = _run_bench(["--gpus", "4", "--steps", "1"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0
+    assert "WORLD_SIZE=2 but --gpus 4" in r.stderr
+    assert '"metric"' not in r.stdout

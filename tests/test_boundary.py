@@ -99,3 +99,35 @@ def test_sd1_config_instantiates_unchanged(sdk):
     assert abs(n / 1e6 - 859.52) < 0.01, n
     assert len(unet.state_dict()) == 686
     assert type(unet).__module__ == "sd_amd.openai_model.model"
+
+
+REF_YAML = "/root/reference/Diffusion/config.yaml"
+
+
+@pytest.mark.skipif(not os.path.exists(REF_YAML), reason="reference checkout not present (GPU box)")
+def test_repo_yaml_equals_reference_config_model_section():
+    """configs/sd-v1-txt2img.yaml holds the reference's Diffusion/config.yaml `model` section key
+    for key, value for value (parsed with yaml.safe_load)."""
+    import yaml
+    mine = yaml.safe_load(open(os.path.join(ROOT, "configs", "sd-v1-txt2img.yaml")))
+    ref = yaml.safe_load(open(REF_YAML))
+    assert mine["model"] == ref["model"]
+
+
+def test_full_latent_diffusion_from_yaml(sdk):
+    """The whole reference model config instantiates through the mirrored resolver: LatentDiffusion
+    with DiffusionWrapper(UNetModel), AutoEncoderKL and the FrozenCLIPEmbedder cond stage
+    (``clip_encoder`` is mirrored), schedule buffers on the host."""
+    import yaml
+    from sd_amd.Diffusion.utils import instantiate_from_config
+    cfg = yaml.safe_load(open(os.path.join(ROOT, "configs", "sd-v1-txt2img.yaml")))
+    with torch.device("meta"):
+        ld = instantiate_from_config(cfg["model"])
+    assert type(ld).__module__ == "sd_amd.Diffusion.ddpm"
+    assert type(ld.model.diffusion_model).__module__ == "sd_amd.openai_model.model"
+    assert type(ld.first_stage_model).__module__ == "sd_amd.VAE.autoencoder"
+    assert type(ld.cond_stage_model).__module__ == "sd_amd.clip_encoder.modules"
+    assert ld.model.conditioning_key == "crossattn" and ld.parameterization == "eps"
+    assert ld.scale_factor == 0.18215 and ld.num_timesteps == 1000
+    assert ld.alphas_cumprod.device.type == "cpu"
+    assert abs(sum(p.numel() for p in ld.model.parameters()) / 1e6 - 859.52) < 0.01

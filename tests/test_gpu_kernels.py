@@ -44,17 +44,14 @@ def _conv_ref(x_nhwc, w, b, stride=1, pad=1, upsample=False, gn=None, silu=False
 
 @pytest.fixture(params=["auto", "0", "2", "3", "4", "5", "6", "7", "8", "9", "16", "17", "18", "19", "20", "21",
                         "22", "23", "24", "25", "26"])
-def conv_variant(request):
+def conv_variant(request, sdk):
     """Every conv kernel variant (register-staged 128x128, LDS-DMA 256x256/256x128/128x128)."""
-    import os
-    old = os.environ.get("SDK_CONV_VARIANT")
+    from sd_amd import ops as o
+    old = o.FORCE_VARIANT
     if request.param != "auto":
-        os.environ["SDK_CONV_VARIANT"] = request.param
+        o.FORCE_VARIANT = int(request.param)
     yield request.param
-    if old is None:
-        os.environ.pop("SDK_CONV_VARIANT", None)
-    else:
-        os.environ["SDK_CONV_VARIANT"] = old
+    o.FORCE_VARIANT = old
 
 
 @pytest.mark.parametrize("B,H,W,Cin,Cout,k,stride,up", [
