@@ -74,8 +74,15 @@ __global__ void __launch_bounds__(NW * 64, QB == 2 ? 1 : 2) attn_fwd_kernel(Attn
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 31, fh = lane >> 5;
-  const int head = blockIdx.y, b = blockIdx.z;
-  const int q0 = blockIdx.x * (32 * QB * NW) + wave * 32 * QB;      // this wave's first query row
+  // 1-D grid, XCD-aware: the q-blocks of one (batch, head) are consecutive logical blocks and
+  // xcd_remap puts consecutive logical blocks on one XCD, so that head's K/V is fetched into one
+  // L2 instead of into all eight (blocks are dealt round-robin over the XCDs)
+  constexpr int ROWS = 32 * QB * NW;
+  const int nqb = (p.nq + ROWS - 1) / ROWS;
+  const int lin = xcd_remap((int)blockIdx.x, (int)gridDim.x);
+  const int qblk = lin % nqb, bh = lin / nqb;
+  const int head = bh % p.heads, b = bh / p.heads;
+  const int q0 = qblk * ROWS + wave * 32 * QB;      // this wave's first query row
   const int d = p.d, nch = (d + 7) >> 3;   // real 16-B chunks per row
   const bool ones_row = d < DV;            // row sum from the PV MFMA (ones column at d)
 
@@ -153,7 +160,7 @@ __global__ void __launch_bounds__(NW * 64, QB == 2 ? 1 : 2) attn_fwd_kernel(Attn
   for (int qb = 0; qb < QB; ++qb) { m_run[qb] = 0.f; l_run[qb] = 0.f; negm[qb] = f16v{}; }
   int ntiles = (p.nk + KT - 1) / KT;
   if constexpr (CAUSAL) {   // tiles past the workgroup's last query row hold only masked keys
-    const int qlast = min(p.nq, (int)(blockIdx.x + 1) * (32 * QB * NW)) - 1;
+    const int qlast = min(p.nq, (qblk + 1) * ROWS) - 1;
     ntiles = min(ntiles, qlast / KT + 1);
   }
 
@@ -318,7 +325,9 @@ __global__ void __launch_bounds__(NW * 64, QB == 2 ? 1 : 2) attn_fwd_kernel(Attn
 template <int DQK, int DV, int NW, int QB>
 int launch(const AttnParams& p, hipStream_t s) {
   constexpr int ROWS = 32 * QB * NW;
-  dim3 grid((p.nq + ROWS - 1) / ROWS, p.heads, p.batch);
+  const long long blocks = (long long)((p.nq + ROWS - 1) / ROWS) * p.heads * p.batch;
+  if (blocks > 0x7fffffffLL) return fail(SDK_EINVAL, "attention: grid too large");
+  dim3 grid((unsigned)blocks);
   if (p.causal) {
     if constexpr (QB == 1) {   // the CLIP text tower's head sizes; other forms are not instantiated
       hipLaunchKernelGGL((attn_fwd_kernel<DQK, DV, NW, QB, true>), grid, dim3(NW * 64), 0, s, p);

@@ -1060,6 +1060,24 @@ __device__ __forceinline__ void epi_vec_store(const EpiVec& e, float* vec_s, int
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
+// Work-item order (xcd_remap then puts consecutive items on one XCD, sharing its L2).  Without
+// split-K: M-tile major — the N-tiles of one pixel panel share its A rows.  With split-K (the
+// 16x16 / 8x8 UNet levels: M = 1024-4096 rows against a 15-60 MB weight matrix) the weight slice
+// is the large operand: (N-tile, K-slice) major, M-tile minor, so the M-tiles that read one weight
+// slice are co-resident on an XCD and the slice comes from L2 instead of once per M-tile.
+__device__ __forceinline__ void item_coords(const Params& p, int it, int& tm, int& tn, int& sidx) {
+  if (p.split == 1) {
+    tm = it / p.tiles_n;
+    tn = it - tm * p.tiles_n;
+    sidx = 0;
+    return;
+  }
+  const int slab = it / p.tiles_m;
+  tm = it - slab * p.tiles_m;
+  tn = slab / p.split;
+  sidx = slab - tn * p.split;
+}
+
 // One (tile, K-split) work item per workgroup, two LDS stages.
 template <class CF>
 __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_glds_kernel(Params p) {
@@ -1071,8 +1089,8 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_glds_kernel(Params p)
   const int nitems = p.tiles_m * p.tiles_n * p.split;
   // XCD-aware item order: neighbouring tiles (shared A rows / W rows) share an L2
   const int it = xcd_remap((int)blockIdx.x + (int)blockIdx.y * (int)gridDim.x, nitems);
-  const int tile = it / p.split, sidx = it - tile * p.split;
-  const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+  int tm, tn, sidx;
+  item_coords(p, it, tm, tn, sidx);
   const int m0 = tm * CF::TBM, n0 = tn * CF::TBN;
   const int kt0 = sidx * p.kt_per_split, kt1 = min(p.kt_total, kt0 + p.kt_per_split);
   const int lrow = lane >> 3;
@@ -1402,8 +1420,8 @@ __global__ void __launch_bounds__(512) conv_ph_kernel(Params p) {
   const int wr = wave >> 2, wc = wave & 3;
   const int nitems = p.tiles_m * p.tiles_n * p.split;
   const int it = xcd_remap((int)blockIdx.x + (int)blockIdx.y * (int)gridDim.x, nitems);
-  const int tile = it / p.split, sidx = it - tile * p.split;
-  const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+  int tm, tn, sidx;
+  item_coords(p, it, tm, tn, sidx);
   const int m0 = tm * 256, n0 = tn * 256;
   const int kt0 = sidx * p.kt_per_split, kt1 = min(p.kt_total, kt0 + p.kt_per_split);
   const int nk = kt1 - kt0;

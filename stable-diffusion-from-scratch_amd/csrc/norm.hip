@@ -9,6 +9,7 @@
 // for offset activations); pass 2 merges chunks in double per channel and
 // channels into groups with Chan's parallel-variance formula.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -177,6 +178,101 @@ __global__ void __launch_bounds__(256) gn_finalize_kernel(const half_t* s0, cons
     scale[(size_t)b * channels + c] = sc;
     shift[(size_t)b * channels + c] = bt - meanf * sc;
   }
+}
+
+// Single-launch GroupNorm statistics for the UNet's small levels (hw <= 4096 pixels per image),
+// where the two-kernel form is latency-bound (partial + finalize ~17 us of kernel time at 8x8
+// for 2.6 MB).  grid (slices, batch): one workgroup owns ONE image and a slice of `gps` whole
+// groups (gps*cg channels, a multiple of 8), streams all its pixels (thread = 8 channels of every
+// rp-th pixel, pivot-shifted fp32 sums, 4 loads in flight), reduces the rp partial rows through
+// LDS, merges channels into groups with Chan's formula in double and writes scale/shift — no
+// workspace, no second launch.
+constexpr int GNF_T = 256;
+__global__ void __launch_bounds__(GNF_T) gn_stats_fused_kernel(const half_t* s0, const half_t* s1, int c_split,
+                                                               int ld0, int ld1, int hw, int channels, int cg,
+                                                               int gps, float eps, const float* gamma,
+                                                               const float* beta, float* scale, float* shift) {
+  __shared__ float2 red[GNF_T * 8];                 // [row-set][slice channel] partial (S1, S2)
+  __shared__ double cmean[GNF_T * 2], cm2[GNF_T * 2];  // per slice channel (slice <= 512 channels)
+  const int tid = threadIdx.x, b = blockIdx.y;
+  const int sc = gps * cg, c0 = blockIdx.x * sc;     // slice channels, first channel
+  const int cv = sc / 8, rp = GNF_T / cv;            // vectors per pixel, pixels in parallel
+  const int v = tid % cv, r0 = tid / cv;
+  const bool active = r0 < rp;
+  const size_t img = (size_t)b * hw;
+  const int c = c0 + 8 * v;
+  float sum[8], sq[8], piv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sum[j] = 0.f; sq[j] = 0.f; piv[j] = 0.f; }
+  if (active) {
+    const h8 pv = load_px(s0, s1, c_split, ld0, ld1, img, c);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) piv[j] = (float)pv[j];
+    constexpr int U = 4;
+    for (int r = r0; r < hw; r += U * rp) {
+      h8 x[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int rr = r + u * rp;
+        x[u] = rr < hw ? load_px(s0, s1, c_split, ld0, ld1, img + rr, c) : pv;   // the pivot adds 0
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = (float)x[u][j] - piv[j];
+          sum[j] += d;
+          sq[j] += d * d;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[r0 * sc + 8 * v + j] = make_float2(sum[j], sq[j]);
+  }
+  __syncthreads();
+  const double n = (double)hw;
+  for (int k = tid; k < sc; k += GNF_T) {           // per slice channel: merge the rp row sets
+    double a1 = 0.0, a2 = 0.0;
+    for (int r = 0; r < rp; ++r) {
+      const float2 q = red[r * sc + k];
+      a1 += q.x;
+      a2 += q.y;
+    }
+    const int cc = c0 + k;
+    const float p0 = cc < c_split ? (float)s0[img * ld0 + cc] : (float)s1[img * ld1 + (cc - c_split)];
+    cmean[k] = (double)p0 + a1 / n;
+    cm2[k] = a2 - a1 * a1 / n;
+  }
+  __syncthreads();
+  for (int g = tid; g < gps; g += GNF_T) {          // per group: Chan merge of its cg channels
+    double ms = 0.0, m2 = 0.0;
+    for (int k = 0; k < cg; ++k) ms += cmean[g * cg + k];
+    const double mg = ms / cg;
+    for (int k = 0; k < cg; ++k) {
+      const double dm = cmean[g * cg + k] - mg;
+      m2 += cm2[g * cg + k] + n * dm * dm;
+    }
+    const double var = (m2 > 0 ? m2 : 0.0) / (n * cg);
+    cmean[g * cg] = mg;                              // reuse: group mean / rstd at the group's first slot
+    cm2[g * cg] = 1.0 / sqrt(var + (double)eps);
+  }
+  __syncthreads();
+  for (int k = tid; k < sc; k += GNF_T) {
+    const int g = k / cg, cc = c0 + k;
+    const float rstd = (float)cm2[g * cg], meanf = (float)cmean[g * cg];
+    const float gm = gamma ? gamma[cc] : 1.f, bt = beta ? beta[cc] : 0.f;
+    const float s = gm * rstd;
+    scale[(size_t)b * channels + cc] = s;
+    shift[(size_t)b * channels + cc] = bt - meanf * s;
+  }
+}
+
+// slice size of the single-launch statistics: the fewest whole groups whose channels are a
+// multiple of 8 (16-B loads), at most 512 channels; 0 = not applicable
+int gn_fused_gps(int channels, int groups) {
+  const int cg = channels / groups;
+  for (int g = 1; g <= groups; ++g)
+    if (groups % g == 0 && (g * cg) % 8 == 0) return g * cg <= 512 ? g : 0;
+  return 0;
 }
 
 // GroupNorm apply (+ SiLU): y = silu?(x*scale[b,c] + shift[b,c]), 8 channels per thread,
@@ -359,6 +455,13 @@ __global__ void __launch_bounds__(256) layer_norm_kernel(const half_t* x, half_t
 
 using namespace sdk;
 
+// largest pixels-per-image for the single-launch statistics (SDK_GN_FUSED_MAX_HW, read at load;
+// measured crossover on MI355X: tools/bench_norm.py)
+static const int g_gn_fused_max_hw = [] {
+  const char* e = getenv("SDK_GN_FUSED_MAX_HW");
+  return e ? atoi(e) : 1024;
+}();
+
 extern "C" int64_t sdk_group_norm_workspace(int32_t batch, int32_t hw, int32_t channels) {
   if (batch <= 0 || hw <= 0 || channels <= 0) return 0;
   GnGeom g = gn_geom(batch, hw, channels);
@@ -373,10 +476,17 @@ extern "C" int sdk_group_norm_affine(const sdk_group_norm_args* a, sdk_stream_t 
   if (a->c_split < a->channels && !a->src1) return fail(SDK_EINVAL, "group_norm: concat without src1");
   if (a->ld0 % 8 || (a->c_split < a->channels && a->ld1 % 8)) return fail(SDK_EINVAL, "group_norm: ld % 8");
   if (a->channels / 8 > 512) return fail(SDK_EINVAL, "group_norm: channels > 4096");
+  hipStream_t s = (hipStream_t)stream;
+  const int gps = gn_fused_gps(a->channels, a->groups);
+  if (gps > 0 && a->hw <= g_gn_fused_max_hw) {
+    hipLaunchKernelGGL(gn_stats_fused_kernel, dim3(a->groups / gps, a->batch), dim3(GNF_T), 0, s,
+                       (const half_t*)a->src0, (const half_t*)a->src1, a->c_split, a->ld0, a->ld1, a->hw, a->channels,
+                       a->channels / a->groups, gps, a->eps, a->gamma, a->beta, a->scale, a->shift);
+    return check_launch("gn_stats_fused");
+  }
   const int64_t need = sdk_group_norm_workspace(a->batch, a->hw, a->channels);
   if (!a->workspace || a->workspace_bytes < need) return fail(SDK_EWORKSPACE, "group_norm: workspace too small");
   GnGeom g = gn_geom(a->batch, a->hw, a->channels);
-  hipStream_t s = (hipStream_t)stream;
   const size_t lds = g.ry > 1 ? (size_t)2 * g.ry * g.c8 * 8 * sizeof(float) : 0;
   hipLaunchKernelGGL(gn_partial_kernel, dim3(g.nchunks, a->batch), dim3(256), lds, s, (const half_t*)a->src0,
                      (const half_t*)a->src1, a->c_split, a->ld0, a->ld1, a->hw, a->channels, g,

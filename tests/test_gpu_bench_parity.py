@@ -114,11 +114,11 @@ def test_bench_config_deterministic(bench_c3):
 
 
 def test_bench_config_short_sample_and_decode_deterministic(bench_c3):
-    """The bench's own one_step (3 DDIM steps + decode, graph replay) twice: bitwise equal images."""
+    """The bench's own one_step (4 DDIM steps + decode, graph replay) twice: bitwise equal images."""
     bench, ld = bench_c3["bench"], bench_c3["ld"]
     from sd_amd.DDIM.ddim import DDIMSampler
     xT, ctx = bench_c3["xT"][:4].contiguous(), bench_c3["ctx"][:4].contiguous()
-    step = bench.make_one_step(DDIMSampler(ld), ld, xT, ctx, 3, 1, None)
+    step = bench.make_one_step(DDIMSampler(ld), ld, xT, ctx, 4, 1, None)
     a = step().clone()
     b = step().clone()
     assert a.shape == (4, 3, 512, 512)
@@ -157,7 +157,7 @@ def test_two_prompts_on_one_model(sdk, graphs):
 
     def run(ld, c):
         s = DDIMSampler(ld)
-        return s.sample(S=3, batch_size=2, shape=(4, 16, 16), conditioning=c, eta=0.0, x_T=xT, verbose=False,
+        return s.sample(S=4, batch_size=2, shape=(4, 16, 16), conditioning=c, eta=0.0, x_T=xT, verbose=False,
                         unconditional_guidance_scale=5.0, unconditional_conditioning=uc)[0].clone()
 
     ld, _ = _tiny_ld(graphs)

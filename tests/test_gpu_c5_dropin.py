@@ -188,7 +188,7 @@ def test_dropin_chain_vs_reference_sampler_golden(sdk, graphs):
 
 def test_dropin_chain_with_text_conditioning_vs_oracle(sdk):
     """Token ids → get_learned_conditioning (HIP CLIP text tower from the YAML's cond stage target)
-    → 3-step DDIM with classifier-free guidance through apply_model → decode, vs the oracle chain
+    → 4-step DDIM with classifier-free guidance through apply_model → decode, vs the oracle chain
     (clip_ref → unet_ref in sampler_ref.ddim_sample → vae_ref)."""
     from oracle.clip_ref import clip_text_forward
     from oracle.sampler_ref import ddim_sample
@@ -219,7 +219,7 @@ def test_dropin_chain_with_text_conditioning_vs_oracle(sdk):
     assert cc.shape == (2, 77, ccfg["hidden_size"])
     g = torch.Generator().manual_seed(31)
     xT = torch.randn(2, 4, 16, 16, generator=g)
-    z, _ = DDIMSampler(ld).sample(S=3, batch_size=2, shape=(4, 16, 16), conditioning=cc, eta=0.0, x_T=xT.to(DEV),
+    z, _ = DDIMSampler(ld).sample(S=4, batch_size=2, shape=(4, 16, 16), conditioning=cc, eta=0.0, x_T=xT.to(DEV),
                                   verbose=False, unconditional_guidance_scale=7.5, unconditional_conditioning=uc)
     img = ld.decode_first_stage(z)
 
@@ -227,7 +227,7 @@ def test_dropin_chain_with_text_conditioning_vs_oracle(sdk):
     rc = clip_text_forward(csd, ids, heads, prefix="")
     ru = clip_text_forward(csd, ids_u, heads, prefix="")
     assert rel_l2(cc, rc) < 1e-2
-    zr, _ = ddim_sample(lambda x, t: unet_forward(usd, ucfg, x, t, rc), xT, 3, guidance_scale=7.5,
+    zr, _ = ddim_sample(lambda x, t: unet_forward(usd, ucfg, x, t, rc), xT, 4, guidance_scale=7.5,
                         uncond_fn=lambda x, t: unet_forward(usd, ucfg, x, t, ru))
     ir = decode_first_stage(vsd, cfg_of(v), zr, 0.18215)
     assert rel_l2(z, zr) < 2e-2

@@ -160,7 +160,8 @@ def test_conv_nchw_f32_out(ops, conv_variant):
     assert rel_l2(y, ref) < 2e-3
 
 
-@pytest.mark.parametrize("C,HW", [(320, 4096), (2560, 64), (128, 16384), (960, 256)])
+@pytest.mark.parametrize("C,HW", [(320, 4096), (2560, 64), (128, 16384), (960, 256), (640, 1024), (1280, 256),
+                                  (1920, 256), (320, 1024), (64, 100)])
 def test_group_norm_stats(ops, C, HW):
     B = 2
     x = (_rand(B, HW, 1, C, seed=7).float() * 2 + 3).half()       # offset activations

@@ -9,8 +9,9 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-SHAPES = [("sd1_64x64", 16, 4096, 320, 40), ("sd1_32x32", 16, 1024, 640, 80), ("sd2_64x64", 16, 4096, 320, 64),
-          ("sd2_32x32", 16, 1024, 640, 64), ("sd1_64x64_cfg", 32, 4096, 320, 40)]
+SHAPES = [("sd1_64x64", 16, 4096, 320, 40), ("sd1_32x32", 16, 1024, 640, 80), ("sd1_16x16", 16, 256, 1280, 160),
+          ("sd1_8x8", 16, 64, 1280, 160), ("sd2_64x64", 16, 4096, 320, 64), ("sd2_32x32", 16, 1024, 640, 64),
+          ("sd2_96_64x64", 8, 9216, 320, 64), ("sd1_64x64_cfg", 32, 4096, 320, 40)]
 
 
 def timeit(f, reps=20):
@@ -30,7 +31,10 @@ def main():
     sd_amd_loader.load()
     from sd_amd import ops
     nk = 77
+    only = sys.argv[sys.argv.index("--only") + 1].split(",") if "--only" in sys.argv else None
     for name, B, N, C, D in SHAPES:
+        if only and name not in only:
+            continue
         H = C // D
         t = torch.randn(B * N, C, device="cuda").half()
         kv = torch.randn(B * nk, 2 * C, device="cuda").half()
@@ -44,11 +48,14 @@ def main():
             q = ops.linear(pcq, t)
             o = ops.attention(q, kv[:, :C], kv[:, C:], batch=B, heads=H, nq=N, nk=nk, head_dim=D, scale=D ** -0.5)
             return ops.linear(pco, o, residual=res)
-        tf, t3 = timeit(fused), timeit(three)
-        flops = 4.0 * B * N * C * C + 4.0 * B * N * nk * C
+        sup = ops.cross_attention_block_supported(C, D, nk, N)
+        tf = timeit(fused) if sup else float("nan")
+        t3 = timeit(three)
+        flops = 4.0 * B * N * C * C + 4.0 * B * N * nk * C       # the block as the reference computes it
         hbm = 3 * B * N * C * 2            # t + residual read, out written
         print(f"{name:16s} B={B:3d} N={N:5d} C={C:4d} d={D:3d}  fused {tf:8.1f} us ({flops / tf / 1e6:7.1f} TFLOP/s, "
-              f"{hbm / tf / 1e6:6.2f} TB/s)   three launches {t3:8.1f} us   speedup {t3 / tf:5.2f}x", flush=True)
+              f"{hbm / tf / 1e6:6.2f} TB/s)   three launches {t3:8.1f} us ({flops / t3 / 1e6:7.1f} TFLOP/s)   "
+              f"speedup {t3 / tf:5.2f}x", flush=True)
 
 
 def phases():
