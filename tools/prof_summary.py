@@ -85,7 +85,7 @@ def main(tag, src=os.path.join(ROOT, "gpurun_out", "prof_round")):
     for fn in (f"{tag}_conv_traffic.json", "conv_traffic.json"):     # the latter is what bench.py reads
         with open(os.path.join(prof, fn), "w") as f:
             json.dump(summ, f, indent=1)
-    for fn in ("shapes.txt", "bench.log"):
+    for fn in ("shapes.txt", "bench.log", "bench_c3.log", "bench_c5.log", "bench_c2.log", "bench_c1.log"):
         p = os.path.join(src, fn)
         if os.path.exists(p):
             shutil.copy(p, os.path.join(prof, f"{tag}_{fn.replace('.txt', '').replace('.log', '')}" +
@@ -94,4 +94,4 @@ def main(tag, src=os.path.join(ROOT, "gpurun_out", "prof_round")):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], *(sys.argv[2:3]))
