@@ -184,16 +184,16 @@ __global__ void __launch_bounds__(256) gn_finalize_kernel(const half_t* s0, cons
 // where the two-kernel form is latency-bound (partial + finalize ~17 us of kernel time at 8x8
 // for 2.6 MB).  grid (slices, batch): one workgroup owns ONE image and a slice of `gps` whole
 // groups (gps*cg channels, a multiple of 8), streams all its pixels (thread = 8 channels of every
-// rp-th pixel, pivot-shifted fp32 sums, 4 loads in flight), reduces the rp partial rows through
+// rp-th pixel, pivot-shifted fp32 sums, 8 loads in flight), reduces the rp partial rows through
 // LDS, merges channels into groups with Chan's formula in double and writes scale/shift — no
 // workspace, no second launch.
-constexpr int GNF_T = 256;
+constexpr int GNF_T = 512;
 __global__ void __launch_bounds__(GNF_T) gn_stats_fused_kernel(const half_t* s0, const half_t* s1, int c_split,
                                                                int ld0, int ld1, int hw, int channels, int cg,
                                                                int gps, float eps, const float* gamma,
                                                                const float* beta, float* scale, float* shift) {
   __shared__ float2 red[GNF_T * 8];                 // [row-set][slice channel] partial (S1, S2)
-  __shared__ double cmean[GNF_T * 2], cm2[GNF_T * 2];  // per slice channel (slice <= 512 channels)
+  __shared__ double cmean[512], cm2[512];           // per slice channel (slice <= 512 channels)
   const int tid = threadIdx.x, b = blockIdx.y;
   const int sc = gps * cg, c0 = blockIdx.x * sc;     // slice channels, first channel
   const int cv = sc / 8, rp = GNF_T / cv;            // vectors per pixel, pixels in parallel
@@ -208,7 +208,7 @@ __global__ void __launch_bounds__(GNF_T) gn_stats_fused_kernel(const half_t* s0,
     const h8 pv = load_px(s0, s1, c_split, ld0, ld1, img, c);
 #pragma unroll
     for (int j = 0; j < 8; ++j) piv[j] = (float)pv[j];
-    constexpr int U = 4;
+    constexpr int U = 8;
     for (int r = r0; r < hw; r += U * rp) {
       h8 x[U];
 #pragma unroll
