@@ -201,6 +201,21 @@ typedef struct {
 int sdk_cross_attention_block_supported(int32_t channels, int32_t head_dim, int32_t nk, int32_t n_img);
 int sdk_cross_attention_block(const sdk_xattn_args* a, sdk_stream_t stream);
 
+/* The same block with BasicTransformerBlock's two LayerNorms around it fused in
+ * (openai_model/attention.py:249-250: x = attn2(norm2(x), context) + x; ... ff(norm3(x))):
+ *  - in_gamma != NULL: a->t holds norm2's INPUT (the token rows, normally a->res as well) and is
+ *    normalised inside the kernel (eps in_eps, fp32 gamma / beta, 16-B aligned);
+ *  - out_gamma != NULL: out_ln[M, out_ln_ld] = norm3(out) is written as well.
+ * Both norms produce the same bits as sdk_layer_norm on the same rows.  Either may be NULL.
+ */
+typedef struct {
+  const float* in_gamma; const float* in_beta; float in_eps;
+  const float* out_gamma; const float* out_beta; float out_eps;
+  void* out_ln; int32_t out_ln_ld;
+} sdk_xattn_ln_args;
+
+int sdk_cross_attention_block_ln(const sdk_xattn_args* a, const sdk_xattn_ln_args* ln, sdk_stream_t stream);
+
 /* ---------------------------------------------------------------- sampler / glue
  * DDIM update (DDIM/ddim.py:194-204 == ldm/diffusion/ddim.py:197-205), fp32,
  * evaluated op by op without contraction so it is bit-identical to torch's CPU

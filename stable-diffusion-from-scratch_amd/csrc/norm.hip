@@ -372,9 +372,9 @@ __global__ void __launch_bounds__(256) gn_apply_ex_kernel(const half_t* s0, cons
 
 // LayerNorm: one wave per row at a time, row cached in registers (cols <= 64*8*LN_MAXV).  Waves
 // walk rows grid-stride with the next row's loads in flight while the current one reduces, gamma /
-// beta live in registers for the whole walk, and mean and variance come out of ONE pair of shuffle
-// chains: sums of (x - x0) and (x - x0)^2 around a pivot x0 taken from the row itself, so the
-// E[d^2] - E[d]^2 form does not cancel (|mean - x0| is of the order of the row's spread).
+// beta live in registers for the whole walk; the row math (one pivot-shifted pair of shuffle
+// chains) is ln_row_stats / ln_apply8 of common.h, shared with the cross-attention block's fused
+// norm2 / norm3.
 constexpr int LN_MAXV = 4;
 template <int MAXV>
 __global__ void __launch_bounds__(256) layer_norm_kernel(const half_t* x, half_t* y, int rows, int cols, int ldx,
@@ -411,42 +411,57 @@ __global__ void __launch_bounds__(256) layer_norm_kernel(const half_t* x, half_t
   for (; row < rows; row += nwaves) {
     h8 nv[MAXV];
     load(row + nwaves, nv);
-    const float x0 = __shfl((float)v[0][0], 0, 64);
-    float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int i = 0; i < MAXV; ++i) {
-      const int k = lane + 64 * i;
-      if (k < c8) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float d = (float)v[i][j] - x0;
-          s1 += d;
-          s2 += d * d;
-        }
-      }
-    }
-    for (int off = 32; off > 0; off >>= 1) {
-      s1 += __shfl_xor(s1, off, 64);
-      s2 += __shfl_xor(s2, off, 64);
-    }
-    const float inv_n = 1.f / cols;
-    const float dm = s1 * inv_n;
-    const float var = fmaxf(s2 * inv_n - dm * dm, 0.f);
-    const float mean = x0 + dm;
-    const float rstd = rsqrtf(var + eps);
+    float mean, rstd;
+    ln_row_stats<MAXV>(v, cols, eps, mean, rstd);
     half_t* yr = y + (size_t)row * ldy;
 #pragma unroll
     for (int i = 0; i < MAXV; ++i) {
       const int k = lane + 64 * i;
-      if (k < c8) {
-        h8 o;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = (half_t)(((float)v[i][j] - mean) * rstd * g[i][j] + bt[i][j]);
-        *reinterpret_cast<h8*>(yr + k * 8) = o;
-      }
+      if (k < c8) *reinterpret_cast<h8*>(yr + k * 8) = ln_apply8(v[i], mean, rstd, g[i], bt[i]);
     }
 #pragma unroll
     for (int i = 0; i < MAXV; ++i) v[i] = nv[i];
+  }
+}
+
+// LayerNorm for C = 32 * CPL (320 / 640: the transformer widths the fused cross-attention block
+// also normalises): 16 rows per wave, four lanes per row (ln_quad_stats, common.h), gamma / beta
+// staged once per block in LDS; waves walk 16-row groups grid-stride with the next group's loads
+// in flight.
+template <int CPL>
+__global__ void __launch_bounds__(256) layer_norm_quad_kernel(const half_t* x, half_t* y, int rows, int ldx, int ldy,
+                                                              const float* gamma, const float* beta, float eps) {
+  constexpr int C = 32 * CPL;
+  __shared__ __attribute__((aligned(16))) float gb[2 * C];
+  for (int e = threadIdx.x; e < C / 4; e += 256) {
+    *reinterpret_cast<f4*>(gb + 4 * e) = *reinterpret_cast<const f4*>(gamma + 4 * e);
+    *reinterpret_cast<f4*>(gb + C + 4 * e) = *reinterpret_cast<const f4*>(beta + 4 * e);
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, q = lane & 3, rl = lane >> 2;
+  const int nwaves = gridDim.x * 4;
+  auto load = [&](int r, h8 (&v)[CPL]) {
+    const half_t* xr = x + (size_t)r * ldx + 8 * q;
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) v[i] = r < rows ? *reinterpret_cast<const h8*>(xr + 32 * i) : h8{};
+  };
+  int r0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
+  h8 v[CPL];
+  load(r0 + rl, v);
+  for (; r0 < rows; r0 += nwaves * 16) {
+    h8 nv[CPL];
+    load(r0 + nwaves * 16 + rl, nv);
+    float mean, rstd;
+    ln_quad_stats<CPL>(v, eps, mean, rstd);
+    const int row = r0 + rl;
+    if (row < rows) {
+      half_t* yr = y + (size_t)row * ldy + 8 * q;
+#pragma unroll
+      for (int i = 0; i < CPL; ++i)
+        *reinterpret_cast<h8*>(yr + 32 * i) = ln_quad_apply(v[i], mean, rstd, gb, C, q + 4 * i);
+    }
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) v[i] = nv[i];
   }
 }
 
@@ -559,7 +574,15 @@ extern "C" int sdk_layer_norm(const void* x, void* y, int32_t rows, int32_t cols
   const int blocks = std::min((rows + 3) / 4, 2048);
   hipStream_t s = (hipStream_t)stream;
   const int c8 = cols / 8;
-  if (c8 <= 64)
+  if (cols == 320 || cols == 640) {
+    const int qblocks = std::min((rows + 63) / 64, 2048);
+    if (cols == 320)
+      hipLaunchKernelGGL(layer_norm_quad_kernel<10>, dim3(qblocks), dim3(256), 0, s, (const half_t*)x, (half_t*)y, rows,
+                         ld_x, ld_y, gamma, beta, eps);
+    else
+      hipLaunchKernelGGL(layer_norm_quad_kernel<20>, dim3(qblocks), dim3(256), 0, s, (const half_t*)x, (half_t*)y, rows,
+                         ld_x, ld_y, gamma, beta, eps);
+  } else if (c8 <= 64)
     hipLaunchKernelGGL(layer_norm_kernel<1>, dim3(blocks), dim3(256), 0, s, (const half_t*)x, (half_t*)y, rows, cols,
                        ld_x, ld_y, gamma, beta, eps);
   else if (c8 <= 128)

@@ -33,6 +33,11 @@ struct XAttnParams {
   int n_img;            // query tokens per image (multiple of 64)
   int nk;               // context tokens (<= 80)
   float c;              // softmax scale * log2(e)
+  // fused LayerNorms (BasicTransformerBlock norm2 / norm3, reference attention.py:249-250), or null
+  // gamma: t is norm2's INPUT and is normalised in LDS; out_ln = norm3(out)
+  const float* ln_in_g; const float* ln_in_b; float ln_in_eps;
+  const float* ln_out_g; const float* ln_out_b; float ln_out_eps;
+  half_t* out_ln; int out_ln_ld;
   unsigned long long* stamps;   // diagnostics (tools/bench_xattn.py --phases): 6 clock stamps per group, or null
 };
 
@@ -114,6 +119,52 @@ __device__ __forceinline__ void proj_wave(const half_t* __restrict__ x, int x_ld
   }
 }
 
+// norm2 / norm3 of the workgroup's 64 rows with the row math of layer_norm_quad_kernel (common.h:
+// the same bits as the separate launch): wave w normalises rows [16w, 16w + 16) of the LDS tile
+// `src`, four lanes per row, gamma / beta read from LDS (`gb`, staged in the K / V^T area, which is
+// free before phase B and after it), and hands every normalised 8-channel chunk to
+// store(row, channel, value).
+template <int C, class Store>
+__device__ __forceinline__ void ln_quad_rows(const half_t* src, int ld, const float* gb, float eps, Store store) {
+  constexpr int CPL = C / 32;
+  const int lane = threadIdx.x & 63, q = lane & 3, row = 16 * (threadIdx.x >> 6) + (lane >> 2);
+  h8 v[CPL];
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) v[i] = *reinterpret_cast<const h8*>(src + row * ld + 8 * (q + 4 * i));
+  float mean, rstd;
+  ln_quad_stats<CPL>(v, eps, mean, rstd);
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    store(row, 8 * (q + 4 * i), ln_quad_apply(v[i], mean, rstd, gb, C, q + 4 * i));
+    // two chunks' gamma / beta reads in flight at a time: hoisting all of them costs the 2nd
+    // resident workgroup (registers)
+    if (i & 1) __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// gamma | beta (fp32, C each) of a fused norm: GBT 16-B pieces per thread, loaded into registers
+// well ahead of use (under the kernel's own HBM stream an L2 miss costs microseconds), then
+// written to the LDS staging area
+template <int C>
+struct LnStage {
+  static constexpr int GBT = (C / 2 + 255) / 256;
+  f4 r[GBT];
+  __device__ __forceinline__ void load(const float* gamma, const float* beta) {
+#pragma unroll
+    for (int u = 0; u < GBT; ++u) {
+      const int e = threadIdx.x + 256 * u;
+      if (e < C / 2) r[u] = *reinterpret_cast<const f4*>(e < C / 4 ? gamma + 4 * e : beta + 4 * (e - C / 4));
+    }
+  }
+  __device__ __forceinline__ void store(float* gb) const {
+#pragma unroll
+    for (int u = 0; u < GBT; ++u) {
+      const int e = threadIdx.x + 256 * u;
+      if (e < C / 2) *reinterpret_cast<f4*>(gb + 4 * e) = r[u];
+    }
+  }
+};
+
 template <int C, int D>
 __global__ void __launch_bounds__(256, 1) xattn_block_kernel(XAttnParams p) {
   using X = XCfg<C, D>;
@@ -126,10 +177,12 @@ __global__ void __launch_bounds__(256, 1) xattn_block_kernel(XAttnParams p) {
   const int b = m0 / p.n_img;
   const int n_w = wave * X::CW;
 
-  // zero: K / V^T padding (keys >= nk, d >= D) and the q pad columns
-  for (int e = tid; e < X::HPI * X::KVH; e += 256) kvl[e] = (half_t)0.f;
+  static_assert(2 * C * 4 <= X::HPI * X::KVH * 2, "norm gamma / beta staging fits the K / V^T area");
+  float* gbl = reinterpret_cast<float*>(kvl);
+  LnStage<C> ln2;
+  if (p.ln_in_g) ln2.load(p.ln_in_g, p.ln_in_b);
+  // zero the q pad columns (the K / V^T padding is zeroed after norm2 has used that area)
   for (int e = tid; e < XQ * 8; e += 256) qo[(e >> 3) * X::QLD + C + (e & 7)] = (half_t)0.f;
-
   stamp(p, 0);
   // ---- phase A: q = t Wq^T -> LDS (fp16, as the separate to_q GEMM stores it).  The t tile is
   // staged into the q buffer first with every 16-B load in flight at once (one HBM latency
@@ -149,8 +202,18 @@ __global__ void __launch_bounds__(256, 1) xattn_block_kernel(XAttnParams p) {
       const int e = tid + 256 * u, row = e / C8, c8 = e - row * C8;
       *reinterpret_cast<h8*>(qo + row * X::QLD + 8 * c8) = tv[u];
     }
+    if (p.ln_in_g) ln2.store(gbl);
   }
   __syncthreads();
+  if (p.ln_in_g) {   // norm2 in place: t = LN(tokens)
+    ln_quad_rows<C>(qo, X::QLD, gbl, p.ln_in_eps,
+                    [&](int row, int c, const h8& v) { *reinterpret_cast<h8*>(qo + row * X::QLD + c) = v; });
+    __syncthreads();
+  }
+  // K / V^T padding (keys >= nk, d >= D) stays zero through phase B; phase A's barriers order this
+  // before the first K / V^T writes
+  static_assert(X::HPI * X::KVH % 8 == 0, "K / V^T area in 16-B pieces");
+  for (int e = tid; e < X::HPI * X::KVH / 8; e += 256) reinterpret_cast<h8*>(kvl)[e] = h8{};
   stamp(p, 1);
   {
     f4 acc[X::NB][4];
@@ -312,6 +375,8 @@ __global__ void __launch_bounds__(256, 1) xattn_block_kernel(XAttnParams p) {
   stamp(p, 3);
   // ---- phase C: out = o Wo^T + bo (fp16) + residual, staged through LDS for row stores
   {
+    LnStage<C> ln3;
+    if (p.out_ln) ln3.load(p.ln_out_g, p.ln_out_b);
     f4 acc[X::NB][4];
     proj_wave<C, X::NB, X::WP>(qo, X::QLD, p.wo, n_w, acc);
     __syncthreads();   // every wave is done reading o
@@ -330,6 +395,7 @@ __global__ void __launch_bounds__(256, 1) xattn_block_kernel(XAttnParams p) {
         *reinterpret_cast<h4v*>(qo + (16 * i + r16) * X::QLD + n) = v;
       }
     }
+    if (p.out_ln) ln3.store(gbl);   // phase B is over: the K / V^T area is free
     __syncthreads();
     constexpr int C8 = C / 8;
     for (int e = tid; e < XQ * C8; e += 256) {
@@ -342,6 +408,14 @@ __global__ void __launch_bounds__(256, 1) xattn_block_kernel(XAttnParams p) {
         for (int q = 0; q < 8; ++q) v[q] = (half_t)((float)v[q] + (float)rr[q]);
       }
       *reinterpret_cast<h8*>(p.out + m * p.out_ld + 8 * c8) = v;
+      if (p.out_ln) *reinterpret_cast<h8*>(qo + row * X::QLD + 8 * c8) = v;
+    }
+    if (p.out_ln) {   // norm3 of the finished rows
+      __syncthreads();
+      half_t* dst = p.out_ln + (size_t)m0 * p.out_ln_ld;
+      const int ld = p.out_ln_ld;
+      ln_quad_rows<C>(qo, X::QLD, gbl, p.ln_out_eps,
+                      [&](int row, int c, const h8& v) { *reinterpret_cast<h8*>(dst + (size_t)row * ld + c) = v; });
     }
   }
   stamp(p, 5);
@@ -372,7 +446,8 @@ extern "C" int sdk_cross_attention_block_supported(int32_t channels, int32_t hea
   return cd && nk >= 1 && nk <= XKP && n_img > 0 && n_img % XQ == 0;
 }
 
-extern "C" int sdk_cross_attention_block(const sdk_xattn_args* a, sdk_stream_t stream) {
+namespace {
+int xattn_run(const sdk_xattn_args* a, const sdk_xattn_ln_args* ln, sdk_stream_t stream) {
   if (!a || !a->t || !a->kv || !a->wq || !a->wo || !a->out) return fail(SDK_EINVAL, "cross_attention_block: null");
   if (!sdk_cross_attention_block_supported(a->channels, a->head_dim, a->nk, a->n_img))
     return fail(SDK_EINVAL, "cross_attention_block: unsupported shape (channels 320/640, head_dim 40/64/80, "
@@ -381,11 +456,40 @@ extern "C" int sdk_cross_attention_block(const sdk_xattn_args* a, sdk_stream_t s
   if (a->t_ld % 8 || a->kv_ld % 8 || a->out_ld % 8 || (a->res && a->res_ld % 8) || a->kv_ld < 2 * a->channels)
     return fail(SDK_EINVAL, "cross_attention_block: row strides must be multiples of 8 (kv >= 2*channels)");
   if (a->w_ld != a->channels) return fail(SDK_EINVAL, "cross_attention_block: weight rows must be channels long");
-  XAttnParams p{(const half_t*)a->t, (const half_t*)a->kv, (const half_t*)a->wq, (const half_t*)a->wo, a->bias,
-                (const half_t*)a->res, (half_t*)a->out, a->t_ld, a->kv_ld, a->res_ld, a->out_ld, a->n_img, a->nk,
-                a->scale * 1.4426950408889634f, g_xattn_stamps};
+  XAttnParams p{};
+  p.t = (const half_t*)a->t; p.kv = (const half_t*)a->kv; p.wq = (const half_t*)a->wq; p.wo = (const half_t*)a->wo;
+  p.bo = a->bias; p.res = (const half_t*)a->res; p.out = (half_t*)a->out;
+  p.t_ld = a->t_ld; p.kv_ld = a->kv_ld; p.res_ld = a->res_ld; p.out_ld = a->out_ld;
+  p.n_img = a->n_img; p.nk = a->nk; p.c = a->scale * 1.4426950408889634f;
+  p.stamps = g_xattn_stamps;
+  if (ln) {
+    if (ln->in_gamma) {
+      if (!ln->in_beta || (((uintptr_t)ln->in_gamma | (uintptr_t)ln->in_beta) & 15))
+        return fail(SDK_EINVAL, "cross_attention_block_ln: norm2 gamma / beta null or not 16-B aligned");
+      p.ln_in_g = ln->in_gamma; p.ln_in_b = ln->in_beta; p.ln_in_eps = ln->in_eps;
+    }
+    if (ln->out_gamma) {
+      if (!ln->out_beta || !ln->out_ln || (((uintptr_t)ln->out_gamma | (uintptr_t)ln->out_beta) & 15))
+        return fail(SDK_EINVAL, "cross_attention_block_ln: norm3 gamma / beta / output null or not 16-B aligned");
+      if (ln->out_ln_ld % 8 || ln->out_ln_ld < a->channels)
+        return fail(SDK_EINVAL, "cross_attention_block_ln: norm3 output row stride");
+      p.ln_out_g = ln->out_gamma; p.ln_out_b = ln->out_beta; p.ln_out_eps = ln->out_eps;
+      p.out_ln = (half_t*)ln->out_ln; p.out_ln_ld = ln->out_ln_ld;
+    }
+  }
   const int m = a->batch * a->n_img;
   hipStream_t s = (hipStream_t)stream;
   if (a->channels == 320) return a->head_dim == 40 ? launch_xattn<320, 40>(p, m, s) : launch_xattn<320, 64>(p, m, s);
   return a->head_dim == 80 ? launch_xattn<640, 80>(p, m, s) : launch_xattn<640, 64>(p, m, s);
+}
+}  // namespace
+
+extern "C" int sdk_cross_attention_block(const sdk_xattn_args* a, sdk_stream_t stream) {
+  return xattn_run(a, nullptr, stream);
+}
+
+extern "C" int sdk_cross_attention_block_ln(const sdk_xattn_args* a, const sdk_xattn_ln_args* ln,
+                                            sdk_stream_t stream) {
+  if (!ln) return fail(SDK_EINVAL, "cross_attention_block_ln: null norm arguments");
+  return xattn_run(a, ln, stream);
 }

@@ -51,6 +51,9 @@ def _ln_prep(ln: nn.LayerNorm, dev):
 _FUSED_ENV = os.environ.get("SD_AMD_FUSED_XATTN")
 FUSED_CROSS_ATTENTION = _FUSED_ENV != "0"
 FUSED_XATTN_MIN_ROWS = 0 if _FUSED_ENV == "1" else 65536
+# norm2 / norm3 folded into that kernel (its prologue / epilogue) instead of two layer_norm launches;
+# SD_AMD_XATTN_NORMS=0 keeps the separate launches (A/B only: the bits are the same)
+FUSED_XATTN_NORMS = os.environ.get("SD_AMD_XATTN_NORMS") != "0"
 
 
 def _use_fused_xattn(channels, head_dim, nk, n_img, batch):
@@ -173,6 +176,17 @@ class BasicTransformerBlock(nn.Module):
     def _run(self, tok, B, N, kv=None, Lc=None):
         t = ops.layer_norm(tok, self.norm1._g, self.norm1._b, self.norm1.eps)
         tok = self.attn1._run(t, tok, B, N)
+        a2 = self.attn2
+        if (kv is not None and FUSED_XATTN_NORMS and tok.stride(-1) == 1
+                and _use_fused_xattn(a2.heads * a2.dim_head, a2.dim_head, Lc, N, B)):
+            # norm2 -> cross-attention -> + residual -> norm3 in one kernel
+            ops.PROFILER.region = "cross_attention"
+            tok, t = ops.cross_attention_block(
+                tok, kv, a2._pc_q, a2._pc_o, batch=B, n_img=N, nk=Lc, heads=a2.heads, head_dim=a2.dim_head,
+                scale=a2.scale, residual=tok, norm_in=(self.norm2._g, self.norm2._b, self.norm2.eps),
+                norm_out=(self.norm3._g, self.norm3._b, self.norm3.eps))
+            ops.PROFILER.region = None
+            return self.ff._run(t, tok)
         t = ops.layer_norm(tok, self.norm2._g, self.norm2._b, self.norm2.eps)
         tok = self.attn2._run(t, tok, B, N, kv, Lc)
         t = ops.layer_norm(tok, self.norm3._g, self.norm3._b, self.norm3.eps)

@@ -15,7 +15,7 @@ import math
 import torch
 
 from . import _lib
-from ._lib import (ACT_NONE, ACT_QUICK_GELU, AttentionArgs, XAttnArgs, ConvArgs, ConvPlanInfo, DdimArgs, GroupNormArgs,
+from ._lib import (ACT_NONE, ACT_QUICK_GELU, AttentionArgs, XAttnArgs, XAttnLnArgs, ConvArgs, ConvPlanInfo, DdimArgs, GroupNormArgs,
                    OUT_GEGLU_F16, OUT_NCHW_F32, OUT_NHWC_F16, OUT_ROWS_F32, check, lib)
 
 BK = 64          # K tile of the conv kernel (packed weight column padding)
@@ -539,9 +539,14 @@ def cross_attention_block_supported(channels, head_dim, nk, n_img):
 
 
 def cross_attention_block(t, kv, pc_q: PackedConv, pc_o: PackedConv, *, batch, n_img, nk, heads, head_dim, scale,
-                          residual=None, out=None):
+                          residual=None, out=None, norm_in=None, norm_out=None, out_ln=None):
     """One-kernel cross-attention block on a cached context K|V: ``to_out(attn(to_q(t), K, V)) + residual``.
-    t / residual: [batch*n_img, C] fp16; kv: [batch*nk, >= 2C] fp16 (K | V)."""
+    t / residual: [batch*n_img, C] fp16; kv: [batch*nk, >= 2C] fp16 (K | V).
+
+    ``norm_in`` = (gamma, beta, eps): ``t`` is the LayerNorm's INPUT and is normalised inside the
+    kernel (BasicTransformerBlock.norm2); ``norm_out`` = (gamma, beta, eps): also returns
+    LayerNorm(out) (norm3) — the result is then ``(out, out_ln)``.  Both match ``layer_norm``
+    bit for bit."""
     Cc = heads * head_dim
     for x, n in ((t, "t"), (kv, "kv")):
         _need_cuda(x, "cross_attention_block " + n)
@@ -563,10 +568,21 @@ def cross_attention_block(t, kv, pc_q: PackedConv, pc_o: PackedConv, *, batch, n
         PROFILER.begin("cross_attention_block", None)
         PROFILER._cur = PROFILER._cur[:2] + (4.0 * batch * n_img * Cc * Cc + 4.0 * batch * n_img * nk * Cc,) + \
             PROFILER._cur[3:]
-    check(lib().sdk_cross_attention_block(C.byref(a), _stream()), "cross_attention_block")
+    if norm_in is None and norm_out is None:
+        check(lib().sdk_cross_attention_block(C.byref(a), _stream()), "cross_attention_block")
+    else:
+        ln = XAttnLnArgs()
+        if norm_in is not None:
+            ln.in_gamma, ln.in_beta, ln.in_eps = norm_in[0].data_ptr(), norm_in[1].data_ptr(), norm_in[2]
+        if norm_out is not None:
+            if out_ln is None:
+                out_ln = torch.empty_like(out)
+            ln.out_gamma, ln.out_beta, ln.out_eps = norm_out[0].data_ptr(), norm_out[1].data_ptr(), norm_out[2]
+            ln.out_ln, ln.out_ln_ld = out_ln.data_ptr(), out_ln.stride(0)
+        check(lib().sdk_cross_attention_block_ln(C.byref(a), C.byref(ln), _stream()), "cross_attention_block")
     if PROFILER.active:
         PROFILER.end()
-    return out
+    return (out, out_ln) if norm_out is not None else out
 
 
 # --------------------------------------------------------------------------- sampler glue

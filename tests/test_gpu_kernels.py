@@ -365,6 +365,51 @@ def test_cross_attention_block(ops, B, N, C, D, nk):
     assert rel_l2(y, y3) < 3e-3
 
 
+@pytest.mark.parametrize("B,N,C,D,nk", [(2, 4096, 320, 40, 77), (2, 1024, 640, 80, 77), (3, 192, 320, 64, 13)])
+def test_cross_attention_block_fused_norms(ops, B, N, C, D, nk):
+    """norm2 / norm3 folded into the cross-attention kernel (sdk_cross_attention_block_ln) give the
+    same bits as layer_norm -> cross_attention_block -> layer_norm, and norm3 matches torch's
+    LayerNorm of the block output."""
+    g = torch.Generator(device="cpu").manual_seed(7 * N + C + nk)
+    H = C // D
+    tok = (torch.randn(B * N, C, generator=g) * 2 + 0.5).half().to(DEV)
+    kv = torch.randn(B * nk, 2 * C, generator=g).half().to(DEV)
+    wq = torch.randn(C, C, generator=g) / math.sqrt(C)
+    wo = torch.randn(C, C, generator=g) / math.sqrt(C)
+    bo = torch.randn(C, generator=g) * 0.1
+    g2, b2 = (1 + 0.1 * torch.randn(C, generator=g)).to(DEV), (0.1 * torch.randn(C, generator=g)).to(DEV)
+    g3, b3 = (1 + 0.1 * torch.randn(C, generator=g)).to(DEV), (0.1 * torch.randn(C, generator=g)).to(DEV)
+    pcq = ops.PackedConv([(wq, C)], None, device=DEV)
+    pco = ops.PackedConv([(wo, C)], bo, device=DEV)
+    kw = dict(batch=B, n_img=N, nk=nk, heads=H, head_dim=D, scale=D ** -0.5)
+    t2 = ops.layer_norm(tok, g2, b2, 1e-5)
+    y_sep = ops.cross_attention_block(t2, kv, pcq, pco, residual=tok, **kw)
+    t3_sep = ops.layer_norm(y_sep, g3, b3, 1e-5)
+    y, t3 = ops.cross_attention_block(tok, kv, pcq, pco, residual=tok, norm_in=(g2, b2, 1e-5),
+                                      norm_out=(g3, b3, 1e-5), **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y_sep)
+    assert torch.equal(t3, t3_sep)
+    ref3 = F.layer_norm(y.float(), (C,), g3, b3, 1e-5)
+    assert rel_l2(t3, ref3) < 2e-3
+    # each norm alone
+    y_in = ops.cross_attention_block(tok, kv, pcq, pco, residual=tok, norm_in=(g2, b2, 1e-5), **kw)
+    assert torch.equal(y_in, y_sep)
+    y_out, t3_out = ops.cross_attention_block(t2, kv, pcq, pco, residual=tok, norm_out=(g3, b3, 1e-5), **kw)
+    assert torch.equal(y_out, y_sep) and torch.equal(t3_out, t3_sep)
+
+
+def test_cross_attention_block_fused_norms_rejects(ops):
+    C, D, N, nk = 320, 40, 64, 77
+    t = torch.zeros(N, C, dtype=torch.float16, device=DEV)
+    kv = torch.zeros(nk, 2 * C, dtype=torch.float16, device=DEV)
+    pc = ops.PackedConv([(torch.zeros(C, C), C)], None, device=DEV)
+    g = torch.ones(C + 1, device=DEV)
+    with pytest.raises(RuntimeError, match="aligned"):
+        ops.cross_attention_block(t, kv, pc, pc, batch=1, n_img=N, nk=nk, heads=8, head_dim=D, scale=0.1,
+                                  norm_in=(g[1:], g[1:], 1e-5))
+
+
 def test_cross_attention_block_rejects_unsupported(ops):
     assert not ops.cross_attention_block_supported(1280, 160, 77, 256)
     assert not ops.cross_attention_block_supported(320, 40, 81, 4096)

@@ -11,7 +11,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 SHAPES = [("sd1_64x64", 16, 4096, 320, 40), ("sd1_32x32", 16, 1024, 640, 80), ("sd1_16x16", 16, 256, 1280, 160),
           ("sd1_8x8", 16, 64, 1280, 160), ("sd2_64x64", 16, 4096, 320, 64), ("sd2_32x32", 16, 1024, 640, 64),
-          ("sd2_96_64x64", 8, 9216, 320, 64), ("sd1_64x64_cfg", 32, 4096, 320, 40)]
+          ("sd2_96_64x64", 8, 9216, 320, 64), ("sd1_64x64_cfg", 32, 4096, 320, 40),
+          ("sd1_32x32_cfg", 32, 1024, 640, 80), ("sd2_96_cfg_96x96", 16, 9216, 320, 64),
+          ("sd2_96_cfg_48x48", 16, 2304, 640, 64)]
 
 
 def timeit(f, reps=20):
@@ -49,6 +51,32 @@ def main():
             o = ops.attention(q, kv[:, :C], kv[:, C:], batch=B, heads=H, nq=N, nk=nk, head_dim=D, scale=D ** -0.5)
             return ops.linear(pco, o, residual=res)
         sup = ops.cross_attention_block_supported(C, D, nk, N)
+        if "--norms" in sys.argv:
+            # norm2 -> block -> norm3: folded into the kernel vs two layer_norm launches around it
+            if not sup:
+                continue
+            g, b = torch.ones(C, device="cuda"), torch.zeros(C, device="cuda")
+            t3 = torch.empty_like(t)
+            folded = lambda: ops.cross_attention_block(res, kv, pcq, pco, batch=B, n_img=N, nk=nk, heads=H,
+                                                       head_dim=D, scale=D ** -0.5, residual=res, norm_in=(g, b, 1e-5),
+                                                       norm_out=(g, b, 1e-5), out_ln=t3)
+
+            def separate():
+                t2 = ops.layer_norm(res, g, b, 1e-5, out=t)
+                y = ops.cross_attention_block(t2, kv, pcq, pco, batch=B, n_img=N, nk=nk, heads=H, head_dim=D,
+                                              scale=D ** -0.5, residual=res)
+                return ops.layer_norm(y, g, b, 1e-5, out=t3)
+            def separate3():
+                t2 = ops.layer_norm(res, g, b, 1e-5, out=t)
+                q = ops.linear(pcq, t2)
+                o = ops.attention(q, kv[:, :C], kv[:, C:], batch=B, heads=H, nq=N, nk=nk, head_dim=D, scale=D ** -0.5)
+                y = ops.linear(pco, o, residual=res)
+                return ops.layer_norm(y, g, b, 1e-5, out=t3)
+            tn, ts, tb, t3l = timeit(folded), timeit(separate), timeit(fused), timeit(separate3)
+            print(f"{name:16s} B={B:3d} N={N:5d} C={C:4d} d={D:3d}  norms folded {tn:8.1f} us   LN + block + LN "
+                  f"{ts:8.1f} us (block alone {tb:8.1f})   LN + three launches + LN {t3l:8.1f} us   "
+                  f"speedup vs best {min(ts, t3l) / tn:5.2f}x", flush=True)
+            continue
         tf = timeit(fused) if sup else float("nan")
         t3 = timeit(three)
         flops = 4.0 * B * N * C * C + 4.0 * B * N * nk * C       # the block as the reference computes it
@@ -68,6 +96,8 @@ def phases():
     nk = 77
     names = ["t stage", "q proj", "heads", "o proj", "store"]
     for name, B, N, C, D in SHAPES:
+        if not ops.cross_attention_block_supported(C, D, nk, N):
+            continue
         H = C // D
         t = torch.randn(B * N, C, device="cuda").half()
         kv = torch.randn(B * nk, 2 * C, device="cuda").half()
@@ -77,8 +107,12 @@ def phases():
         groups = B * N // 64
         st = torch.zeros(groups * 8, dtype=torch.int64, device="cuda")
         lib().sdk_xattn_debug_stamps(ctypes.c_void_p(st.data_ptr()))
+        kw = {}
+        if "--norms" in sys.argv:   # norm2 counts into "t stage", norm3 into "store"
+            g, b = torch.ones(C, device="cuda"), torch.zeros(C, device="cuda")
+            kw = dict(norm_in=(g, b, 1e-5), norm_out=(g, b, 1e-5))
         ops.cross_attention_block(t, kv, pcq, pco, batch=B, n_img=N, nk=nk, heads=H, head_dim=D, scale=D ** -0.5,
-                                  residual=res)
+                                  residual=res, **kw)
         torch.cuda.synchronize()
         lib().sdk_xattn_debug_stamps(None)
         s = st.view(groups, 8)[:, :6].double().cpu()
