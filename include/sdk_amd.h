@@ -98,6 +98,10 @@ typedef struct {
   int64_t workspace_bytes;
   int32_t variant_hint;    /* 0 = choose; 1 + variant id forces a tile configuration (autotuning) */
   int32_t act;             /* enum sdk_conv_act: applied after bias / row_bias, before the residual */
+  float* gn_partial;       /* NULL, or GroupNorm statistics of the fp16 NHWC output (only when the plan's
+                              gn_chunks > 0): [batch][gn_chunks][cout] float pairs (mean, M2) over
+                              ho*wo/gn_chunks output pixels each — sdk_group_norm merges them instead of
+                              a statistics pass over the tensor */
 } sdk_conv_args;
 
 enum sdk_conv_act {
@@ -111,6 +115,7 @@ typedef struct {
   int64_t workspace_bytes;
   int32_t variant;         /* kernel variant id (sdk_kernel_name); split_k > 1 adds splitk_reduce_kernel */
   double flops;            /* algorithmic 2*M*N*K over the unpadded K */
+  int32_t gn_chunks;       /* > 0: the plan can emit GroupNorm statistics (sdk_conv_args.gn_partial) */
 } sdk_conv_plan_info;
 
 int sdk_conv2d_plan(const sdk_conv_args* a, sdk_conv_plan_info* info);
@@ -148,6 +153,17 @@ int sdk_group_norm_apply(const sdk_group_norm_args* a, int32_t silu, void* y, in
  * (no per-tap masks — the zero padding of nn.Conv2d(padding=1) is stored, not computed). */
 int sdk_group_norm_apply_padded(const sdk_group_norm_args* a, int32_t silu, void* y, int32_t ld_y, int32_t h,
                                 int32_t w, int32_t pad, sdk_stream_t stream);
+
+/* GroupNorm (+ SiLU) end to end — the whole GroupNorm32 / Normalize module + nn.SiLU of the call
+ * sites above: y = silu?(x*scale + shift) into y [batch][h+2*pad][w+2*pad][ld_y] (pad 0: contiguous).
+ * Statistics: merged from the per-chunk channel statistics the producing sdk_conv2d emitted
+ * (sdk_conv_args.gn_partial; part0 = source 0's [batch][nch0][c_split], part1 = source 1's
+ * [batch][nch1][channels - c_split] for a concat; NULL = none), else computed from x (one fused
+ * statistics + apply launch at hw <= 64).  a->scale / a->shift / a->workspace as for
+ * sdk_group_norm_affine (the fused launch does not touch them). */
+int sdk_group_norm(const sdk_group_norm_args* a, int32_t silu, void* y, int32_t ld_y, int32_t h, int32_t w,
+                   int32_t pad, const float* part0, int32_t nch0, const float* part1, int32_t nch1,
+                   sdk_stream_t stream);
 
 /* The post-activation GroupNorm of the DDPM (config C1) UNet (DDPM/models/layers.py:23-38 ConvBlock,
  * :311-338 ResNetBlock, :154 attention post-norm): y = [silu](x*scale + shift) + post_bias[b][c]

@@ -19,7 +19,7 @@ from torch import nn
 
 from .. import ops
 from ..Unet.attention import make_attention
-from ..Unet.unet import Downsample, Normalize, ResnetBlock, Upsample, _gn_prep, gn_stats
+from ..Unet.unet import Downsample, Normalize, ResnetBlock, Upsample, _gn_prep, gn_act
 
 
 class Encoder(nn.Module):
@@ -102,7 +102,7 @@ class Encoder(nn.Module):
         h = self.mid.attn_1._run(h)
         h = self.mid.block_2._run(h)
         gp, cp = ops.gn_conv_pad()
-        ha = ops.group_norm_apply(h, gn_stats(self.norm_out, h), silu=True, pad=gp)
+        ha = gn_act(self.norm_out, h, silu=True, pad=gp)
         return ops.conv2d(self._pc_out, ha, pad=cp, out_mode=ops.OUT_NCHW_F32)
 
     @torch.no_grad()
@@ -191,7 +191,7 @@ class Decoder(nn.Module):
         if self.tanh_out:
             raise NotImplementedError("sd_amd: tanh_out is not on the SD path")
         gp, cp = ops.gn_conv_pad()
-        ha = ops.group_norm_apply(h, gn_stats(self.norm_out, h), silu=True, pad=gp)
+        ha = gn_act(self.norm_out, h, silu=True, pad=gp)
         return ops.conv2d(self._pc_out, ha, pad=cp, out_mode=ops.OUT_NCHW_F32)
 
     @torch.no_grad()

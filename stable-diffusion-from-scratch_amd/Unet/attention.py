@@ -11,7 +11,7 @@ import torch
 from torch import nn
 
 from .. import ops
-from .unet import _gn_prep, gn_stats
+from .unet import _gn_prep, gn_act
 
 
 class FlashAttentionBlock(nn.Module):
@@ -36,7 +36,7 @@ class FlashAttentionBlock(nn.Module):
 
     def _run(self, x):
         B, H, W, C = x.shape
-        xn = ops.group_norm_apply(x, gn_stats(self.norm, x), silu=False)
+        xn = gn_act(self.norm, x, silu=False)
         qkv = ops.conv2d(self._pc_qkv, xn).view(B * H * W, 3 * C)
         o = ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], batch=B, heads=self.num_heads, nq=H * W,
                           nk=H * W, head_dim=self.head_dim, scale=self.head_dim ** -0.5)

@@ -28,6 +28,11 @@ def gn_stats(gn, x):
     return ops.group_norm_affine(x, gn._g, gn._b, gn.eps, gn.num_groups)
 
 
+def gn_act(gn, x, silu=True, pad=0):
+    """Normalize (+ nonlinearity) of x materialised, zero-bordered by ``pad`` (``sdk_group_norm``)."""
+    return ops.group_norm(x, gn._g, gn._b, gn.eps, gn.num_groups, silu=silu, pad=pad)
+
+
 class Upsample(nn.Module):
     def __init__(self, in_channels, with_conv):
         super().__init__()
@@ -107,8 +112,8 @@ class ResnetBlock(nn.Module):
             raise NotImplementedError("sd_amd: the VAE ResnetBlock path has no timestep embedding")
         # zero-bordered GN+SiLU outputs: both 3x3 convs run with pad 0 (mask-free gather)
         gp, cp = ops.gn_conv_pad()
-        h = ops.conv2d(self._pc1, ops.group_norm_apply(x, gn_stats(self.norm1, x), silu=True, pad=gp), pad=cp)
-        ha = ops.group_norm_apply(h, gn_stats(self.norm2, h), silu=True, pad=gp)
+        h = ops.conv2d(self._pc1, gn_act(self.norm1, x, silu=True, pad=gp), pad=cp)
+        ha = gn_act(self.norm2, h, silu=True, pad=gp)
         if self._mode == "identity":
             return ops.conv2d(self._pc2, ha, pad=cp, residual=x)
         if self._mode == "fused":

@@ -19,6 +19,7 @@
 // fused with the residual add.  Low-parallelism shapes (the 16x16 / 8x8 UNet
 // levels) split K across workgroups into fp32 slabs reduced by a second kernel.
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 #include "common.h"
@@ -64,6 +65,8 @@ struct Params {
                         // variant 0), so the LDS-DMA kernels' epilogues carry no activation code
   int nomask;           // segment 0 has every tap in range (pad 0, no pad_end / upsample, cin % 64 == 0):
                         // the LDS-DMA A gather is a lane base + a scalar tap offset, no masks
+  float2* gnp;          // GroupNorm statistics of the fp16 output: [batch][gn_nch][N] (mean, M2) over
+  int gn_nch;           // hw_out / gn_nch rows each (one chunk = one M-tile, or 64 rows of the split-K reduce)
 };
 
 // epilogue activation (CLIP's quick_gelu x*sigmoid(1.702x), transformers activations.py QuickGELUActivation)
@@ -518,11 +521,108 @@ __device__ __forceinline__ void epilogue_direct(const Params& p, f16v (&acc)[FM]
 constexpr int EPI_RS = 72;                 // scratch row stride (halfs) = 144 B
 constexpr int EPI_BYTES = 32 * EPI_RS * 2;  // per-wave scratch
 
+// ---------------------------------------------------------------------- GroupNorm statistics in the epilogue
+// The convs that produce a GroupNorm input (ResBlock conv1 / conv2, Down/Upsample, proj_out, conv_in)
+// emit per-channel statistics of the fp16 values they store (after bias / embedding / residual),
+// so GroupNorm needs no statistics pass over the tensor: per (image, M-tile, channel) the tile's
+// (mean, M2) — Chan's parallel form; sdk_group_norm merges the tiles and the group's channels in
+// double.  Register-free design (the 16-wave tiles run at a 128-VGPR cap): the epilogue's read-back
+// writes the final values back into the wave's LDS scratch block, then a column pass reads the
+// block per channel pair (exact two-pass mean / M2 over a few rows in registers), merges the lane
+// row slices with xor shuffles (equal counts) and parks one pair per (row block, channel) in the
+// wave's scratch; after the epilogue one thread per tile channel merges its column's blocks.
+//
+// Column pass over a block of ROWS x CH fp16 values at `blk` (row stride RS halfs); writes
+// dst[c] = (mean, M2) for c < CH.
+template <int ROWS, int CH, int RS>
+__device__ __forceinline__ void gn_block_stats(const half_t* blk, float2* dst) {
+  constexpr int CP = CH / 2, SL = 64 / CP, RPL = ROWS / SL;   // channel pairs, row slices, rows per lane
+  static_assert(CP * SL == 64 && RPL * SL == ROWS, "block shape");
+  const int lane = threadIdx.x & 63, cp = lane % CP, sl = lane / CP;
+  const half_t* col = blk + sl * RPL * RS + 2 * cp;
+  // two passes over the lane's rows (the second re-reads LDS instead of holding 2*RPL floats)
+  float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+  for (int k = 0; k < RPL; ++k) {
+    const h2 v = *reinterpret_cast<const h2*>(col + k * RS);
+    a0 += (float)v[0];
+    a1 += (float)v[1];
+  }
+  float m0 = a0 * (1.f / RPL), m1 = a1 * (1.f / RPL), q0 = 0.f, q1 = 0.f;
+#pragma unroll
+  for (int k = 0; k < RPL; ++k) {
+    const h2 v = *reinterpret_cast<const h2*>(col + k * RS);
+    const float d0 = (float)v[0] - m0, d1 = (float)v[1] - m1;
+    q0 = fmaf(d0, d0, q0);
+    q1 = fmaf(d1, d1, q1);
+  }
+  float n = (float)RPL;
+#pragma unroll
+  for (int off = CP; off < 64; off <<= 1) {          // equal counts: mean = average, M2 += d^2 n/2
+    const float mb0 = __shfl_xor(m0, off, 64), qb0 = __shfl_xor(q0, off, 64);
+    const float mb1 = __shfl_xor(m1, off, 64), qb1 = __shfl_xor(q1, off, 64);
+    const float d0 = mb0 - m0, d1 = mb1 - m1;
+    m0 = 0.5f * (m0 + mb0);
+    m1 = 0.5f * (m1 + mb1);
+    q0 += qb0 + d0 * d0 * (0.5f * n);
+    q1 += qb1 + d1 * d1 * (0.5f * n);
+    n *= 2.f;
+  }
+  if (lane < CP) {
+    dst[2 * cp] = make_float2(m0, q0);
+    dst[2 * cp + 1] = make_float2(m1, q1);
+  }
+}
+
+// after every wave parked its blocks: one thread per tile channel merges the WM waves x NBLK row
+// blocks (BR rows each) of its column and stores the tile's pair; `wave_stats(w)` = wave w's
+// parked array [NBLK][TN]
+template <int WM, int WN, int TN, int NBLK, int BR, int TBM, int TBN, class F>
+__device__ __forceinline__ void gn_tile_store(const Params& p, int m0, int n0, F wave_stats) {
+  const int t = threadIdx.x;
+  if (t >= TBN || n0 + t >= p.N) return;
+  const int wn = t / TN, c = t - wn * TN;
+  float2 r = make_float2(0.f, 0.f);
+  float n = 0.f;
+#pragma unroll
+  for (int wm = 0; wm < WM; ++wm)
+#pragma unroll
+    for (int k = 0; k < NBLK; ++k) {
+      const float2 b = wave_stats(wm * WN + wn)[k * TN + c];
+      const float dl = b.x - r.x, f = (float)BR / (n + (float)BR);
+      r.x += dl * f;
+      r.y += b.y + dl * dl * n * f;
+      n += (float)BR;
+    }
+  const int b0 = m0 / p.hw_out, chunk = (m0 - b0 * p.hw_out) / TBM;
+  p.gnp[((size_t)b0 * p.gn_nch + chunk) * p.N + n0 + t] = r;
+}
+
+// split-K reduce: a lane's pivot-shifted sums over its rows (registers are plentiful there)
+struct GnAcc {
+  float piv[8], s1[8], s2[8];
+};
+
+__device__ __forceinline__ void gn_acc_add(GnAcc& a, const h8& v, bool first) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float x = (float)v[j];
+    if (first) {
+      a.piv[j] = x;
+      a.s1[j] = 0.f;
+      a.s2[j] = 0.f;
+    }
+    const float d = x - a.piv[j];
+    a.s1[j] += d;
+    a.s2[j] = fmaf(d, d, a.s2[j]);
+  }
+}
+
 // Bias and the timestep-embedding row (row_bias of the tile's image) are staged in LDS once per
 // workgroup (stage_epi_vectors, before the K loop): the epilogue reads them with ds_read instead of
 // waiting on a global load per 32-row block.  ``bias_s`` / ``rb_s`` = nullptr fall back to global.
 // Residual rows are loaded one block ahead (issued before the current block's LDS round trip).
-template <int FM, int FN>
+template <int FM, int FN, bool GN = false>
 __device__ __forceinline__ void epilogue_lds(const Params& p, f16v (&acc)[FM][FN], int m0, int n0, int m_w, int n_w,
                                              half_t* wbuf, const float* bias_s = nullptr,
                                              const float* rb_s = nullptr) {
@@ -579,10 +679,13 @@ __device__ __forceinline__ void epilogue_lds(const Params& p, f16v (&acc)[FM][FN
   }
   // fp16 NHWC: blocks (i, jp) of 32 pixels x (32|64) channels, flattened so the residual rows of
   // block q+1 are in flight while block q makes its LDS round trip
+  // channel-block major (jp outer, 32-pixel block i inner): one block's GN statistics live at a time
   constexpr int NJP = (FN + 1) / 2, NBLK = FM * NJP;
   h8 rcur[4], rnext[4];
+  constexpr int TN = FN * 32;
+  float2* gst = reinterpret_cast<float2*>(wbuf + EPI_BYTES / 2);   // GN: parked [FM][TN] (mean, M2)
   auto block_geom = [&](int q, int& mt, int& nb, int& nt) __attribute__((always_inline)) {
-    const int i = q / NJP, jp = (q - i * NJP) * 2;
+    const int jp = (q / FM) * 2, i = q % FM;
     mt = m0 + m_w + i * 32;
     nb = n0 + n_w + jp * 32;
     nt = (FN - jp >= 2) ? 2 : 1;
@@ -607,7 +710,7 @@ __device__ __forceinline__ void epilogue_lds(const Params& p, f16v (&acc)[FM][FN
   for (int q = 0; q < NBLK; ++q) {
     int mt, nb, nt;
     block_geom(q, mt, nb, nt);
-    const int i = q / NJP, jp = (q - i * NJP) * 2;
+    const int jp = (q / FM) * 2, i = q % FM;
     if (p.res && AHEAD && q + 1 < NBLK) load_res(q + 1, rnext);
     if (p.res && !AHEAD) load_res(q, rcur);
     if (mt < p.M && nb < p.N) {
@@ -660,13 +763,16 @@ __device__ __forceinline__ void epilogue_lds(const Params& p, f16v (&acc)[FM][FN
         const int row = r * rpi + lane / lpr, c8 = lane % lpr;
         h8 v = *reinterpret_cast<const h8*>(wbuf + row * EPI_RS + c8 * 8);
         const int m = mt + row, n = nb + c8 * 8;
-        if (m < p.M && n < p.N) {
-          if (p.res) {
+        if (p.res) {
 #pragma unroll
-            for (int qq = 0; qq < 8; ++qq) v[qq] = (half_t)((float)v[qq] + (float)rcur[r][qq]);
-          }
-          *reinterpret_cast<h8*>(out + (size_t)m * p.out_ld + n) = v;
+          for (int qq = 0; qq < 8; ++qq) v[qq] = (half_t)((float)v[qq] + (float)rcur[r][qq]);
         }
+        if constexpr (GN) *reinterpret_cast<h8*>(wbuf + row * EPI_RS + c8 * 8) = v;   // final values for the stats
+        if (m < p.M && n < p.N) *reinterpret_cast<h8*>(out + (size_t)m * p.out_ld + n) = v;
+      }
+      if constexpr (GN) {   // full tiles only: every row stored
+        if (nt == 2) gn_block_stats<32, 64, EPI_RS>(wbuf, gst + i * TN + jp * 32);
+        else gn_block_stats<32, 32, EPI_RS>(wbuf, gst + i * TN + jp * 32);
       }
     }
     if (p.res && AHEAD && q + 1 < NBLK) {
@@ -702,9 +808,10 @@ __device__ __forceinline__ void epi16_load_res(const Params& p, int mt, int nb, 
   }
 }
 
-template <int NB>
+template <int NB, bool GN = false>
 __device__ __forceinline__ void epi16_group(const Params& p, const f4* a, int mt, int nb, int n0, int bw, bool rb_vec,
-                                            half_t* wbuf, const float* bias_s, const float* rb_s, const h8 (&rr)[2]) {
+                                            half_t* wbuf, const float* bias_s, const float* rb_s, const h8 (&rr)[2],
+                                            float2* gdst = nullptr) {
   const int lane = threadIdx.x & 63, px = lane & 15, cg = lane >> 4;
   half_t* out = reinterpret_cast<half_t*>(p.out);
   auto bias4 = [&](int n) __attribute__((always_inline)) {
@@ -780,18 +887,19 @@ __device__ __forceinline__ void epi16_group(const Params& p, const f4* a, int mt
     const int row = r * RPI + lane / LPR, c8 = lane % LPR;
     h8 v = *reinterpret_cast<const h8*>(wbuf + row * EPG_RS + c8 * 8);
     const int m = mt + row, n = nb + c8 * 8;
-    if (m < p.M && n < p.N) {
-      if (p.res) {
+    if (p.res) {
 #pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = (half_t)((float)v[q] + (float)rr[r][q]);
-      }
-      *reinterpret_cast<h8*>(out + (size_t)m * p.out_ld + n) = v;
+      for (int q = 0; q < 8; ++q) v[q] = (half_t)((float)v[q] + (float)rr[r][q]);
     }
+    if constexpr (GN) *reinterpret_cast<h8*>(wbuf + row * EPG_RS + c8 * 8) = v;   // final values for the stats
+    if (m < p.M && n < p.N) *reinterpret_cast<h8*>(out + (size_t)m * p.out_ld + n) = v;
   }
+  if constexpr (GN) gn_block_stats<16, 16 * NB, EPG_RS>(wbuf, gdst);   // full tiles only: every row stored
 }
 
 // groups (i, g) flattened; the residual rows of group q+1 are loaded while group q is written
-template <int FM, int FN>
+// (GN: per-channel statistics of the stored values, parked at wbuf + EPG_BYTES — gn_tile_store)
+template <int FM, int FN, bool GN = false>
 __device__ __forceinline__ void epilogue16_tile(const Params& p, f4 (&acc)[FM][FN], int m0, int n0, int m_w, int n_w,
                                                 half_t* wbuf, const float* bias_s = nullptr,
                                                 const float* rb_s = nullptr) {
@@ -800,8 +908,10 @@ __device__ __forceinline__ void epilogue16_tile(const Params& p, f4 (&acc)[FM][F
   constexpr int NG = FN / 4 + (FN % 4 == 2 ? 1 : 0), NQ = FM * NG;
   constexpr bool AHEAD = FM * FN * 4 + 16 <= 96;
   h8 rcur[2], rnext[2];
+  constexpr int TN = FN * 16;
+  float2* gst = reinterpret_cast<float2*>(wbuf + EPG_BYTES / 2);   // GN: parked [FM][TN] (mean, M2)
   auto load = [&](int q, h8 (&rr)[2]) __attribute__((always_inline)) {
-    const int i = q / NG, g = q - i * NG;
+    const int g = q / FM, i = q - g * FM;
     const int mt = m0 + m_w + 16 * i;
     if (g < FN / 4) epi16_load_res<4>(p, mt, n0 + n_w + 64 * g, rr);
     else epi16_load_res<2>(p, mt, n0 + n_w + 16 * (FN - 2), rr);
@@ -809,16 +919,18 @@ __device__ __forceinline__ void epilogue16_tile(const Params& p, f4 (&acc)[FM][F
   if (p.res && AHEAD) load(0, rcur);
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
-    const int i = q / NG, g = q - i * NG;
+    const int g = q / FM, i = q - g * FM;
     if (p.res && AHEAD && q + 1 < NQ) load(q + 1, rnext);
     if (p.res && !AHEAD) load(q, rcur);
     const int mt = m0 + m_w + 16 * i;
     if (mt < p.M) {
       const int bw = min(mt + px, p.M - 1) / p.hw_out;
       if (g < FN / 4)
-        epi16_group<4>(p, &acc[i][4 * g], mt, n0 + n_w + 64 * g, n0, bw, rb_vec, wbuf, bias_s, rb_s, rcur);
+        epi16_group<4, GN>(p, &acc[i][4 * g], mt, n0 + n_w + 64 * g, n0, bw, rb_vec, wbuf, bias_s, rb_s, rcur,
+                           gst + i * TN + 64 * g);
       else
-        epi16_group<2>(p, &acc[i][FN - 2], mt, n0 + n_w + 16 * (FN - 2), n0, bw, rb_vec, wbuf, bias_s, rb_s, rcur);
+        epi16_group<2, GN>(p, &acc[i][FN - 2], mt, n0 + n_w + 16 * (FN - 2), n0, bw, rb_vec, wbuf, bias_s, rb_s,
+                           rcur, gst + i * TN + 64 * g);
     }
     if (p.res && AHEAD && q + 1 < NQ) {
       rcur[0] = rnext[0];
@@ -873,11 +985,12 @@ __device__ __forceinline__ void epilogue16_tile_direct(const Params& p, f4 (&acc
 // applied by gn_apply before 3x3 convs); every segment must be transform-free.
 __device__ __attribute__((aligned(16))) half_t g_zero_page[8];
 
-template <int BM_, int BN_, int WM_, int WN_, int NS_ = 2, bool M16_ = false>
+template <int BM_, int BN_, int WM_, int WN_, int NS_ = 2, bool M16_ = false, int OCC_ = 1>
 struct Cfg {
   static constexpr int TBM = BM_, TBN = BN_, WM = WM_, WN = WN_;
   static constexpr int NS = NS_;                         // LDS ring stages (NS - 1 K-steps of DMA in flight)
   static constexpr bool M16 = M16_;                      // v_mfma_f32_16x16x32_f16 instead of 32x32x16
+  static constexpr int OCC = OCC_;                       // workgroups meant to share a CU (LDS and VGPR budget)
   static constexpr int NW = WM * WN, NT = NW * 64;
   static constexpr int TM = TBM / WM, TN = TBN / WN;
   static constexpr int FM = TM / 32, FN = TN / 32;
@@ -890,8 +1003,8 @@ struct Cfg {
   static_assert(TBM % 8 == 0 && TBN % 8 == 0, "A/B boundary must align to an 8-row piece");
   static constexpr int RING_BYTES = NS * STAGE_H * 2 + (GPW * NW > NINSTR ? 1024 : 0);  // + dummy slot
   static constexpr int LDS_BYTES = RING_BYTES + 2 * TBN * 4;   // + staged bias / embedding row
-  static_assert(LDS_BYTES <= 160 * 1024, "the ring must fit the 160 KiB LDS");
-  static_assert(RING_BYTES / NW >= EPI_BYTES, "per-wave epilogue scratch");
+  static_assert(LDS_BYTES * OCC <= 160 * 1024, "OCC rings must fit the 160 KiB LDS");
+  static_assert(RING_BYTES / NW >= EPI_BYTES + TM / 16 * TN * 8, "per-wave epilogue scratch + parked GN statistics");
   static_assert(TBN <= NT, "one staged bias element per thread");
 };
 
@@ -1080,7 +1193,7 @@ __device__ __forceinline__ void item_coords(const Params& p, int it, int& tm, in
 
 // One (tile, K-split) work item per workgroup, two LDS stages.
 template <class CF>
-__global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_glds_kernel(Params p) {
+__global__ void __launch_bounds__(CF::NT, CF::OCC * CF::NW / 4) conv_glds_kernel(Params p) {
   extern __shared__ __attribute__((aligned(16))) half_t lds[];
   constexpr int GPW = CF::GPW;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1214,19 +1327,35 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_glds_kernel(Params p)
   __builtin_amdgcn_s_barrier();
   const float* bias_s = p.bias ? vec_s : nullptr;
   const float* rb_s = ev.one_img ? vec_s + CF::TBN : nullptr;
+  constexpr int WSCR = CF::RING_BYTES / CF::NW / 16 * 8;   // per-wave epilogue scratch (halfs)
+  half_t* wscr = lds + wave * WSCR;
+  const bool lds_epi = p.split == 1 && (p.out_mode == SDK_OUT_NHWC_F16 || p.out_mode == SDK_OUT_GEGLU_F16);
+  // the tile's GroupNorm statistics (build_params enables p.gnp for full fp16 NHWC tiles only)
+  auto gn_store = [&](int scratch_halfs, auto blk_rows) __attribute__((always_inline)) {
+    constexpr int BR = decltype(blk_rows)::value;
+    __syncthreads();
+    gn_tile_store<CF::WM, CF::WN, CF::TN, CF::TM / BR, BR, CF::TBM, CF::TBN>(
+        p, m0, n0, [&](int w) { return reinterpret_cast<const float2*>(lds + w * WSCR + scratch_halfs); });
+  };
   if constexpr (CF::M16) {
-    if (p.split == 1 && (p.out_mode == SDK_OUT_NHWC_F16 || p.out_mode == SDK_OUT_GEGLU_F16))
-      epilogue16_tile<CF::FM16, CF::FN16>(p, acc16, m0, n0, wm * CF::TM, wn * CF::TN,
-                                          lds + wave * (CF::RING_BYTES / CF::NW / 16 * 8), bias_s, rb_s);
-    else
+    if (lds_epi && p.gnp) {
+      epilogue16_tile<CF::FM16, CF::FN16, true>(p, acc16, m0, n0, wm * CF::TM, wn * CF::TN, wscr, bias_s, rb_s);
+      gn_store(EPG_BYTES / 2, std::integral_constant<int, 16>{});
+    } else if (lds_epi) {
+      epilogue16_tile<CF::FM16, CF::FN16>(p, acc16, m0, n0, wm * CF::TM, wn * CF::TN, wscr, bias_s, rb_s);
+    } else {
       epilogue16_tile_direct<CF::FM16, CF::FN16>(p, acc16, m0, n0, wm * CF::TM, wn * CF::TN, sidx);
+    }
     return;
   }
-  if (p.split == 1 && (p.out_mode == SDK_OUT_NHWC_F16 || p.out_mode == SDK_OUT_GEGLU_F16))
-    epilogue_lds<CF::FM, CF::FN>(p, acc, m0, n0, wm * CF::TM, wn * CF::TN,
-                                 lds + wave * (CF::RING_BYTES / CF::NW / 16 * 8), bias_s, rb_s);
-  else
+  if (lds_epi && p.gnp) {
+    epilogue_lds<CF::FM, CF::FN, true>(p, acc, m0, n0, wm * CF::TM, wn * CF::TN, wscr, bias_s, rb_s);
+    gn_store(EPI_BYTES / 2, std::integral_constant<int, 32>{});
+  } else if (lds_epi) {
+    epilogue_lds<CF::FM, CF::FN>(p, acc, m0, n0, wm * CF::TM, wn * CF::TN, wscr, bias_s, rb_s);
+  } else {
     epilogue_direct<CF::FM, CF::FN>(p, acc, m0, n0, wm * CF::TM, wn * CF::TN, sidx);
+  }
 }
 
 using Cfg256x256 = Cfg<256, 256, 2, 4>;
@@ -1249,6 +1378,11 @@ using Cfg128x320m = Cfg<128, 320, 4, 2, 2, true>;
 using Cfg256x160m = Cfg<256, 160, 8, 1, 2, true>;
 using Cfg128x256r3m = Cfg<128, 256, 2, 4, 3, true>;
 using Cfg128x128r3m = Cfg<128, 128, 2, 2, 3, true>;
+// short-K token GEMMs (K = 320-1280): two workgroups per CU, so one's epilogue (store drain) runs
+// under the other's K loop — a 2-stage 128x160 / 128x128 ring is 74 / 65 KiB
+using Cfg128x160o2m = Cfg<128, 160, 4, 1, 2, true, 2>;
+using Cfg128x128o2m = Cfg<128, 128, 2, 2, 2, true, 2>;
+using Cfg128x160r4m = Cfg<128, 160, 4, 1, 4, true>;      // one workgroup, 3 K-steps of DMA in flight
 
 
 // ---------------------------------------------------------------------- 16x16x32 epilogues
@@ -1720,6 +1854,67 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(Params p) {
   }
 }
 
+// Split-K reduction + epilogue that also emits the GroupNorm statistics of its rows (p.gnp):
+// grid (batch * gn_nch, ceil(N / 64)); 256 threads = 32 row lanes x 8 column octets over one chunk
+// (hw_out / gn_nch rows of one image); per-lane pivot-shifted sums, Chan merge of the 32 row lanes
+// through LDS, one (mean, M2) per chunk and channel.
+__global__ void __launch_bounds__(256) splitk_reduce_gn_kernel(Params p) {
+  __shared__ float2 red[32][64];
+  const int tc = threadIdx.x & 7, tr = threadIdx.x >> 3;
+  const int b = blockIdx.x / p.gn_nch, chunk = blockIdx.x - b * p.gn_nch;
+  const int R = p.hw_out / p.gn_nch;
+  const int n = blockIdx.y * 64 + tc * 8;
+  const bool colok = n < p.N;
+  GnAcc ga;
+  for (int r = tr; r < R && colok; r += 32) {
+    const int m = b * p.hw_out + chunk * R + r;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = 0.f;
+    for (int sp = 0; sp < p.split; ++sp) {
+      const f4* src = reinterpret_cast<const f4*>(p.partial + ((size_t)sp * p.M + m) * p.Npad + n);
+      const f4 a = src[0], c = src[1];
+      v[0] += a[0]; v[1] += a[1]; v[2] += a[2]; v[3] += a[3];
+      v[4] += c[0]; v[5] += c[1]; v[6] += c[2]; v[7] += c[3];
+    }
+    h8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (p.bias) v[j] += p.bias[n + j];
+      if (p.row_bias) v[j] += p.row_bias[(size_t)b * p.rb_ld + n + j];
+      o[j] = (half_t)act_fn(p.act, v[j]);
+    }
+    if (p.res) {
+      const h8 rr = ldg16(p.res + (size_t)m * p.res_ld + n);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (half_t)((float)o[j] + (float)rr[j]);
+    }
+    *reinterpret_cast<h8*>(reinterpret_cast<half_t*>(p.out) + (size_t)m * p.out_ld + n) = o;
+    gn_acc_add(ga, o, r == tr);
+  }
+  const int cnt = R > tr ? (R - tr + 31) / 32 : 0;
+  if (cnt > 0 && colok) {
+    const float inv = 1.f / (float)cnt;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      red[tr][tc * 8 + j] = make_float2(ga.piv[j] + ga.s1[j] * inv, fmaxf(ga.s2[j] - ga.s1[j] * ga.s1[j] * inv, 0.f));
+  }
+  __syncthreads();
+  const int c = threadIdx.x, nn = blockIdx.y * 64 + c;
+  if (c >= 64 || nn >= p.N) return;
+  float2 acc = red[0][c];
+  float na = (float)((R + 31) / 32);
+  for (int t = 1; t < 32 && t < R; ++t) {
+    const float nb = (float)((R - t + 31) / 32);
+    const float2 q = red[t][c];
+    const float dl = q.x - acc.x, f = nb / (na + nb);
+    acc.x += dl * f;
+    acc.y += q.y + dl * dl * na * f;
+    na += nb;
+  }
+  p.gnp[((size_t)b * p.gn_nch + chunk) * p.N + nn] = acc;
+}
+
 template <class CF>
 int launch_glds(const Params& p, hipStream_t s) {
   static std::atomic<unsigned long long> attr_set{0};   // per device: the dynamic-LDS cap is raised once
@@ -1861,21 +2056,23 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   const int forced = a->variant_hint > 0 ? a->variant_hint - 1 : g_env_variant;
   // ids: 0 register-staged; 2..7 LDS-DMA configs; 8, 9 phased 256x256; 10..15 diagnostics;
   // 16..19 deep-ring LDS-DMA configs; 20, 21 phased 256x256 on v_mfma_f32_16x16x32_f16;
-  // 22..26 LDS-DMA configs 5, 7, 6, 19, 18 on v_mfma_f32_16x16x32_f16; 27..30 diagnostics.
+  // 22..26 LDS-DMA configs 5, 7, 6, 19, 18 on v_mfma_f32_16x16x32_f16; 27..30 diagnostics;
+  // 31, 32 two-per-CU 128x160 / 128x128 (16x16x32); 33 128x160 with a 4-stage ring.
   // The diagnostic ablations compute wrong outputs by design: the product library rejects them,
   // only the separate diagnostics build (-DSDK_CONV_DIAGNOSTICS, libsdk_amd_diag.so) runs them.
   if (is_diagnostic_variant(forced) && !kDiagnostics)
     return fail(SDK_EINVAL, "conv2d: variant " + std::to_string(forced) +
                                 " is a diagnostic ablation (only in libsdk_amd_diag.so)");
-  if (forced > 30 || forced == 1) return fail(SDK_EINVAL, "conv2d: unknown variant " + std::to_string(forced));
+  if (forced > 33 || forced == 1) return fail(SDK_EINVAL, "conv2d: unknown variant " + std::to_string(forced));
   const int fbase = forced;
-  const bool fvalid = forced >= 0 && forced != 1 && forced <= 30;
-  const bool fgeglu = (fbase <= 4 || fbase >= 8) && fbase != 22 && fbase != 23 && fbase != 24;
+  const bool fvalid = forced >= 0 && forced != 1 && forced <= 33;
+  const bool fgeglu = (fbase <= 4 || fbase >= 8) && fbase != 22 && fbase != 23 && fbase != 24 && fbase != 31 &&
+                      fbase != 33;
   if (fvalid && (forced == 0 || !transform) && (fgeglu || a->out_mode != SDK_OUT_GEGLU_F16)) {
-    static const int fbm[31] = {128, 0, 256, 256, 128, 256, 256, 128, 256, 256, 256, 256, 256, 256, 256, 256,
-                                128, 256, 128, 128, 256, 256, 256, 128, 256, 128, 128, 256, 256, 256, 256};
-    static const int fbn[31] = {128, 0, 256, 128, 128, 320, 160, 320, 256, 256, 256, 256, 256, 256, 256, 256,
-                                128, 128, 128, 256, 256, 256, 320, 320, 160, 256, 128, 256, 256, 256, 256};
+    static const int fbm[34] = {128, 0, 256, 256, 128, 256, 256, 128, 256, 256, 256, 256, 256, 256, 256, 256, 128,
+                                256, 128, 128, 256, 256, 256, 128, 256, 128, 128, 256, 256, 256, 256, 128, 128, 128};
+    static const int fbn[34] = {128, 0, 256, 128, 128, 320, 160, 320, 256, 256, 256, 256, 256, 256, 256, 256, 128,
+                                128, 128, 256, 256, 256, 320, 320, 160, 256, 128, 256, 256, 256, 256, 160, 128, 160};
     var = forced;
     tbm = fbm[fbase];
     tbn = fbn[fbase];
@@ -1886,7 +2083,7 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   p.tiles_n = (p.N + tbn - 1) / tbn;
   p.Npad = p.tiles_n * tbn;                       // split-K slab row stride
   const int tiles = p.tiles_m * p.tiles_n;
-  const int per_cu = (var == 0 || var == 4) ? 2 : 1;
+  const int per_cu = (var == 0 || var == 4 || var == 31 || var == 32) ? 2 : 1;
   int split = a->split_k;
   if (split <= 0) {
     if (best_split > 0) {
@@ -1912,6 +2109,23 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   if (split > 1) {
     if (a->cout % 8) return fail(SDK_EINVAL, "conv2d: split-K needs cout % 8 == 0 (pass split_k = 1)");
     p.partial = a->workspace;
+  }
+  // GroupNorm statistics of the output: chunks per image the plan can emit (0 = none).  Split-K: the
+  // reduce kernel, 64-row chunks (one chunk when hw_out is not a multiple of 64); otherwise the
+  // LDS-DMA kernels' fp16 epilogue, one chunk per M-tile when tiles do not straddle images.
+  const bool glds = (var >= 2 && var <= 7) || (var >= 16 && var <= 19) || (var >= 22 && var <= 26) ||
+                    (var >= 31 && var <= 33);
+  int gn_nch = 0;
+  if (a->out_mode == SDK_OUT_NHWC_F16) {
+    if (split > 1) gn_nch = p.hw_out % 64 == 0 ? p.hw_out / 64 : 1;
+    else if (glds && p.hw_out % tbm == 0) gn_nch = p.hw_out / tbm;
+  }
+  if (info) info->gn_chunks = gn_nch;
+  if (a->gn_partial) {
+    if (gn_nch == 0)
+      return fail(SDK_EINVAL, "conv2d: this plan emits no GroupNorm statistics (sdk_conv_plan_info.gn_chunks == 0)");
+    p.gnp = reinterpret_cast<float2*>(a->gn_partial);
+    p.gn_nch = gn_nch;
   }
   return SDK_OK;
 }
@@ -1963,6 +2177,9 @@ extern "C" int sdk_conv2d(const sdk_conv_args* a, sdk_stream_t stream) {
     case 24: rc = launch_glds<Cfg256x160m>(p, s); break;
     case 25: rc = launch_glds<Cfg128x256r3m>(p, s); break;
     case 26: rc = launch_glds<Cfg128x128r3m>(p, s); break;
+    case 31: rc = launch_glds<Cfg128x160o2m>(p, s); break;
+    case 32: rc = launch_glds<Cfg128x128o2m>(p, s); break;
+    case 33: rc = launch_glds<Cfg128x160r4m>(p, s); break;
 #ifdef SDK_CONV_DIAGNOSTICS
     case 27: rc = launch_ph<PhCfg8, 128>(p, s); break;   // diagnostics: no W DMA issued
     case 28: rc = launch_ph<PhCfg8, 256>(p, s); break;   // diagnostics: no A DMA issued
@@ -1974,7 +2191,10 @@ extern "C" int sdk_conv2d(const sdk_conv_args* a, sdk_stream_t stream) {
       rc = check_launch("conv_igemm");
   }
   if (rc) return rc;
-  if (p.split > 1) {
+  if (p.split > 1 && p.gnp) {
+    hipLaunchKernelGGL(splitk_reduce_gn_kernel, dim3(p.batch * p.gn_nch, (p.N + 63) / 64), dim3(256), 0, s, p);
+    if (int e = check_launch("splitk_reduce_gn")) return e;
+  } else if (p.split > 1) {
     const size_t total = (size_t)p.M * (p.N / 8);
     int blocks = (int)std::min<size_t>((total + 255) / 256, 4096);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, p);

@@ -188,10 +188,15 @@ __global__ void __launch_bounds__(256) gn_finalize_kernel(const half_t* s0, cons
 // LDS, merges channels into groups with Chan's formula in double and writes scale/shift — no
 // workspace, no second launch.
 constexpr int GNF_T = 512;
+// APPLY: the same workgroup then normalises its slice (+ SiLU) straight into y — the image's slice
+// is L2-hot from the statistics sweep — optionally into a zero-bordered [h+2pad][w+2pad] image
+// for a pad-0 3x3 conv; GroupNorm at the small levels is then ONE launch instead of stats + apply.
+template <bool APPLY>
 __global__ void __launch_bounds__(GNF_T) gn_stats_fused_kernel(const half_t* s0, const half_t* s1, int c_split,
                                                                int ld0, int ld1, int hw, int channels, int cg,
                                                                int gps, float eps, const float* gamma,
-                                                               const float* beta, float* scale, float* shift) {
+                                                               const float* beta, float* scale, float* shift,
+                                                               int silu, half_t* y, int ldy, int h, int w, int pad) {
   __shared__ float2 red[GNF_T * 8];                 // [row-set][slice channel] partial (S1, S2)
   __shared__ double cmean[512], cm2[512];           // per slice channel (slice <= 512 channels)
   const int tid = threadIdx.x, b = blockIdx.y;
@@ -261,8 +266,126 @@ __global__ void __launch_bounds__(GNF_T) gn_stats_fused_kernel(const half_t* s0,
     const float rstd = (float)cm2[g * cg], meanf = (float)cmean[g * cg];
     const float gm = gamma ? gamma[cc] : 1.f, bt = beta ? beta[cc] : 0.f;
     const float s = gm * rstd;
-    scale[(size_t)b * channels + cc] = s;
-    shift[(size_t)b * channels + cc] = bt - meanf * s;
+    if constexpr (APPLY) {
+      red[k] = make_float2(s, bt - meanf * s);       // the row sets were merged above: reuse as (scale, shift)
+    } else {
+      scale[(size_t)b * channels + cc] = s;
+      shift[(size_t)b * channels + cc] = bt - meanf * s;
+    }
+  }
+  if constexpr (APPLY) {
+    __syncthreads();
+    if (!active) return;
+    float sa[8], sh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float2 t = red[8 * v + j];
+      sa[j] = t.x;
+      sh[j] = t.y;
+    }
+    const int wp = w + 2 * pad, npix = (h + 2 * pad) * wp;
+    half_t* yb = y + (size_t)b * npix * ldy + c;
+    constexpr int U = 4;
+    for (int r = r0; r < npix; r += U * rp) {
+      h8 x[U];
+      bool in[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int rr = r + u * rp;
+        const int py = rr / wp - pad, px = rr - (rr / wp) * wp - pad;
+        in[u] = rr < npix && (unsigned)py < (unsigned)h && (unsigned)px < (unsigned)w;
+        x[u] = in[u] ? load_px(s0, s1, c_split, ld0, ld1, img + (size_t)py * w + px, c) : h8{};
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int rr = r + u * rp;
+        if (rr >= npix) continue;
+        h8 o = {};
+        if (in[u]) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float t = (float)x[u][j] * sa[j] + sh[j];
+            if (silu) t = t * __builtin_amdgcn_rcpf(1.0f + __expf(-t));
+            o[j] = (half_t)t;
+          }
+        }
+        *reinterpret_cast<h8*>(yb + (size_t)rr * ldy) = o;
+      }
+    }
+  }
+}
+
+// GroupNorm statistics merged from the producing convs' per-chunk channel statistics
+// (sdk_conv_args.gn_partial: [batch][nch][C] (mean, M2) over hw/nch pixels each; one array per
+// concat source) — no pass over the tensor.  grid (groups, batch): per channel a Chan merge of its
+// chunks in double, then wave 0 merges the group's channels as gn_finalize_kernel does.
+__global__ void __launch_bounds__(256) gn_finalize_part_kernel(const float2* part0, int nch0, const float2* part1,
+                                                               int nch1, int c_split, int hw, int channels,
+                                                               int groups, float eps, const float* gamma,
+                                                               const float* beta, float* scale, float* shift) {
+  __shared__ double cm[256], cq[256];   // per-channel mean, M2 over the image (cg <= 256)
+  const int grp = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cg = channels / groups, c0 = grp * cg;
+  // tpc consecutive lanes per channel (power of two, <= 64) take disjoint chunk subsets — all loads
+  // independent — then merge with xor shuffles (Chan, counts carried along)
+  int tpc = 64;
+  while (tpc > 1 && tpc * cg > 256) tpc >>= 1;
+  const int ci = tid / tpc, sub = tid - ci * tpc;
+  for (int cbase = 0; cbase < cg; cbase += 256 / tpc) {
+    const int cc = cbase + ci;
+    const bool act = ci < 256 / tpc && cc < cg;
+    double mean = 0.0, m2 = 0.0, n = 0.0;
+    if (act) {
+      const int c = c0 + cc;
+      const bool second = c >= c_split;
+      const float2* pp = second ? part1 : part0;
+      const int nch = second ? nch1 : nch0, cs = second ? channels - c_split : c_split, cl = second ? c - c_split : c;
+      const double rows = (double)hw / nch;
+      for (int k = sub; k < nch; k += tpc) {
+        const float2 q = pp[((size_t)b * nch + k) * cs + cl];
+        const double dl = (double)q.x - mean, nn = n + rows, f = rows / nn;
+        mean += dl * f;
+        m2 += (double)q.y + dl * dl * n * f;
+        n = nn;
+      }
+    }
+    for (int off = tpc >> 1; off > 0; off >>= 1) {   // lanes of one channel are contiguous and aligned
+      const double mb = __shfl_xor(mean, off, 64), qb = __shfl_xor(m2, off, 64), nb = __shfl_xor(n, off, 64);
+      const double nn = n + nb;
+      if (nn > 0) {
+        const double dl = mb - mean, f = nb / nn;
+        mean += dl * f;
+        m2 += qb + dl * dl * n * f;
+      }
+      n = nn;
+    }
+    if (act && sub == 0) {
+      cm[cc] = mean;
+      cq[cc] = m2;
+    }
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  const double n = (double)hw;
+  double mean_sum = 0.0;
+  for (int ci = lane; ci < cg; ci += 64) mean_sum += cm[ci];
+  mean_sum = wave_sum_d(mean_sum);
+  const double mg = mean_sum / cg;
+  double m2g = 0.0;
+  for (int ci = lane; ci < cg; ci += 64) {
+    const double dm = cm[ci] - mg;
+    m2g += cq[ci] + n * dm * dm;
+  }
+  m2g = wave_sum_d(m2g);
+  const double var = (m2g > 0 ? m2g : 0.0) / (n * cg);
+  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float meanf = (float)mg;
+  for (int ci = lane; ci < cg; ci += 64) {
+    const int c = c0 + ci;
+    const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+    const float sc = gm * rstd;
+    scale[(size_t)b * channels + c] = sc;
+    shift[(size_t)b * channels + c] = bt - meanf * sc;
   }
 }
 
@@ -494,9 +617,10 @@ extern "C" int sdk_group_norm_affine(const sdk_group_norm_args* a, sdk_stream_t 
   hipStream_t s = (hipStream_t)stream;
   const int gps = gn_fused_gps(a->channels, a->groups);
   if (gps > 0 && a->hw <= g_gn_fused_max_hw) {
-    hipLaunchKernelGGL(gn_stats_fused_kernel, dim3(a->groups / gps, a->batch), dim3(GNF_T), 0, s,
+    hipLaunchKernelGGL(gn_stats_fused_kernel<false>, dim3(a->groups / gps, a->batch), dim3(GNF_T), 0, s,
                        (const half_t*)a->src0, (const half_t*)a->src1, a->c_split, a->ld0, a->ld1, a->hw, a->channels,
-                       a->channels / a->groups, gps, a->eps, a->gamma, a->beta, a->scale, a->shift);
+                       a->channels / a->groups, gps, a->eps, a->gamma, a->beta, a->scale, a->shift, 0, nullptr, 0,
+                       0, 0, 0);
     return check_launch("gn_stats_fused");
   }
   const int64_t need = sdk_group_norm_workspace(a->batch, a->hw, a->channels);
@@ -592,4 +716,55 @@ extern "C" int sdk_layer_norm(const void* x, void* y, int32_t rows, int32_t cols
     hipLaunchKernelGGL(layer_norm_kernel<LN_MAXV>, dim3(blocks), dim3(256), 0, s, (const half_t*)x, (half_t*)y, rows,
                        cols, ld_x, ld_y, gamma, beta, eps);
   return check_launch("layer_norm");
+}
+
+// GroupNorm (+ SiLU) end to end: statistics and apply, written contiguous (pad = 0) or into a
+// zero-bordered [B][h+2pad][w+2pad][ld_y] image.  Statistics: merged from the producing convs'
+// per-chunk partials when given (part0, and part1 for a concat), else one fused statistics+apply
+// launch at the smallest levels (hw <= SDK_GN_APPLY_FUSED_MAX_HW), else the statistics pass; then
+// the apply pass.  a->scale / a->shift (and a->workspace for the statistics pass) as for
+// sdk_group_norm_affine.
+static const int g_gn_apply_fused_max_hw = [] {
+  const char* e = getenv("SDK_GN_APPLY_FUSED_MAX_HW");
+  return e ? atoi(e) : 64;
+}();
+
+extern "C" int sdk_group_norm(const sdk_group_norm_args* a, int32_t silu, void* y, int32_t ld_y, int32_t h, int32_t w,
+                              int32_t pad, const float* part0, int32_t nch0, const float* part1, int32_t nch1,
+                              sdk_stream_t stream) {
+  if (!a || !a->src0 || !y) return fail(SDK_EINVAL, "group_norm: null pointer");
+  if (a->channels % 8 || a->groups <= 0 || a->channels % a->groups || a->c_split % 8 || a->c_split <= 0 ||
+      a->c_split > a->channels || ld_y % 8 || ld_y < a->channels)
+    return fail(SDK_EINVAL, "group_norm: channels/c_split/ld_y must be multiples of 8, channels % groups == 0");
+  if (a->channels / a->groups > 256) return fail(SDK_EINVAL, "group_norm: > 256 channels per group");
+  if (a->c_split < a->channels && !a->src1) return fail(SDK_EINVAL, "group_norm: concat without src1");
+  if (a->ld0 % 8 || (a->c_split < a->channels && a->ld1 % 8)) return fail(SDK_EINVAL, "group_norm: ld % 8");
+  if (h <= 0 || w <= 0 || (int64_t)h * w != a->hw || pad < 0 || pad > 4)
+    return fail(SDK_EINVAL, "group_norm: h*w must equal hw, pad in [0, 4]");
+  const bool concat = a->c_split < a->channels;
+  const bool parts = part0 && (!concat || part1);
+  if (parts && (nch0 <= 0 || a->hw % nch0 || (concat && (nch1 <= 0 || a->hw % nch1))))
+    return fail(SDK_EINVAL, "group_norm: partial chunks must divide hw");
+  hipStream_t s = (hipStream_t)stream;
+  const int gps = gn_fused_gps(a->channels, a->groups);
+  if (!parts && gps > 0 && a->hw <= g_gn_apply_fused_max_hw && a->batch > 0) {
+    hipLaunchKernelGGL(gn_stats_fused_kernel<true>, dim3(a->groups / gps, a->batch), dim3(GNF_T), 0, s,
+                       (const half_t*)a->src0, (const half_t*)a->src1, a->c_split, a->ld0, a->ld1, a->hw, a->channels,
+                       a->channels / a->groups, gps, a->eps, a->gamma, a->beta, nullptr, nullptr, silu, (half_t*)y,
+                       ld_y, h, w, pad);
+    return check_launch("gn_fused_apply");
+  }
+  if (!a->scale || !a->shift) return fail(SDK_EINVAL, "group_norm: scale/shift buffers needed");
+  if (parts) {
+    if (a->batch > 0) {
+      hipLaunchKernelGGL(gn_finalize_part_kernel, dim3(a->groups, a->batch), dim3(256), 0, s, (const float2*)part0,
+                         nch0, (const float2*)part1, nch1, a->c_split, a->hw, a->channels, a->groups, a->eps, a->gamma,
+                         a->beta, a->scale, a->shift);
+      if (int e = check_launch("gn_finalize_part")) return e;
+    }
+  } else if (int e = sdk_group_norm_affine(a, stream)) {
+    return e;
+  }
+  return pad ? sdk_group_norm_apply_padded(a, silu, y, ld_y, h, w, pad, stream)
+             : sdk_group_norm_apply(a, silu, y, ld_y, stream);
 }

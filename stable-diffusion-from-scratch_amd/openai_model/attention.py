@@ -38,6 +38,10 @@ def _gn_stats(gn: nn.GroupNorm, x):
     return ops.group_norm_affine(x, gn._g, gn._b, gn.eps, gn.num_groups)
 
 
+def _gn(gn: nn.GroupNorm, x, silu=False):
+    return ops.group_norm(x, gn._g, gn._b, gn.eps, gn.num_groups, silu=silu)
+
+
 def _ln_prep(ln: nn.LayerNorm, dev):
     ln._g = ln.weight.detach().to(dev, torch.float32).contiguous()
     ln._b = ln.bias.detach().to(dev, torch.float32).contiguous()
@@ -222,12 +226,12 @@ class SpatialTransformer(nn.Module):
         B, H, W, Cc = x.shape
         # GN materialised by one streaming pass, then the LDS-DMA GEMM (a GN prologue forces the
         # register-staged kernel: 150-190 TF/s on these shapes vs 330-650 for apply + DMA GEMM)
-        xn = ops.group_norm_apply(x, _gn_stats(self.norm, x), silu=False)
+        xn = _gn(self.norm, x)
         h = ops.conv2d(self._pc_in, xn)
         tok = h.view(B * H * W, self.inner_dim)
         for i, blk in enumerate(self.transformer_blocks):
             tok = blk._run(tok, B, H * W, None if kvs is None else kvs[i], Lc)
-        return ops.conv2d(self._pc_out, tok.view(B, H, W, self.inner_dim), residual=x)
+        return ops.conv2d(self._pc_out, tok.view(B, H, W, self.inner_dim), residual=x, gn_stats=True)
 
 
 class QKVAttentionLegacy(nn.Module):
@@ -279,9 +283,9 @@ class AttentionBlock(nn.Module):
 
     def _run(self, x):
         B, H, W, Cc = x.shape
-        xn = ops.group_norm_apply(x, self.norm.stats(x), silu=False)
+        xn = self.norm.norm(x, silu=False)
         qkv = ops.conv2d(self._pc_qkv, xn).view(B * H * W, 3 * Cc)
         ch = Cc // self.num_heads
         o = ops.attention(qkv[:, :Cc], qkv[:, Cc:2 * Cc], qkv[:, 2 * Cc:], batch=B, heads=self.num_heads,
                           nq=H * W, nk=H * W, head_dim=ch, scale=self.attention.scale(ch))
-        return ops.conv2d(self._pc_proj, o.view(B, H, W, Cc), residual=x)
+        return ops.conv2d(self._pc_proj, o.view(B, H, W, Cc), residual=x, gn_stats=True)

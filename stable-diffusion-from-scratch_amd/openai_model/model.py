@@ -43,7 +43,7 @@ class TimestepEmbedSequential(nn.Sequential, TimestepBlock):
             elif isinstance(layer, (AttentionBlock, Downsample, Upsample)):
                 x = layer._run(x)
             elif isinstance(layer, nn.Conv2d):
-                x = ops.conv2d(layer._pc, x)
+                x = ops.conv2d(layer._pc, x, gn_stats=True)
             else:
                 raise NotImplementedError(f"sd_amd: layer {type(layer).__name__} has no HIP path")
         return x
@@ -67,7 +67,7 @@ class Downsample(nn.Module):
         self._pc = ops.PackedConv([(self.op.weight, self.channels)], self.op.bias, device=dev)
 
     def _run(self, x):
-        return ops.conv2d(self._pc, x, stride=2, pad=self.padding)
+        return ops.conv2d(self._pc, x, stride=2, pad=self.padding, gn_stats=True)
 
 
 class Upsample(nn.Module):
@@ -88,7 +88,7 @@ class Upsample(nn.Module):
         self._pc = ops.PackedConv([(self.conv.weight, self.channels)], self.conv.bias, device=dev)
 
     def _run(self, x):
-        return ops.conv2d(self._pc, x, upsample=True, pad=self.padding)
+        return ops.conv2d(self._pc, x, upsample=True, pad=self.padding, gn_stats=True)
 
 
 class ResBlock(TimestepBlock):
@@ -142,15 +142,15 @@ class ResBlock(TimestepBlock):
     def _run(self, x, emb_all, emb_off):
         # GN+SiLU outputs are written zero-bordered: both 3x3 convs run with pad 0 (mask-free gather)
         gp, cp = ops.gn_conv_pad()
-        xa = ops.group_norm_apply(x, self.in_layers[0].stats(x), silu=True, pad=gp)
-        h = ops.conv2d(self._pc1, xa, pad=cp, row_bias=(emb_all, emb_off))
-        ha = ops.group_norm_apply(h, self.out_layers[0].stats(h), silu=True, pad=gp)
+        xa = self.in_layers[0].norm(x, silu=True, pad=gp)
+        h = ops.conv2d(self._pc1, xa, pad=cp, row_bias=(emb_all, emb_off), gn_stats=True)
+        ha = self.out_layers[0].norm(h, silu=True, pad=gp)
         if self._skip_mode == "identity":
-            return ops.conv2d(self._pc2, ha, pad=cp, residual=x)
+            return ops.conv2d(self._pc2, ha, pad=cp, residual=x, gn_stats=True)
         if self._skip_mode == "fused":
-            return ops.conv2d(self._pc2, ha, pad=cp, seg2=(x, None, False))
+            return ops.conv2d(self._pc2, ha, pad=cp, seg2=(x, None, False), gn_stats=True)
         skip = ops.conv2d(self._pc_skip, x)
-        return ops.conv2d(self._pc2, ha, pad=cp, residual=skip)
+        return ops.conv2d(self._pc2, ha, pad=cp, residual=skip, gn_stats=True)
 
 
 class UNetModel(nn.Module):
@@ -374,6 +374,6 @@ class UNetModel(nn.Module):
         for module in self.output_blocks:
             h = module._run((h, hs.pop()), st)
         gp, cp = ops.gn_conv_pad()
-        ha = ops.group_norm_apply(h, self.out[0].stats(h), silu=True, pad=gp)
+        ha = self.out[0].norm(h, silu=True, pad=gp)
         out = ops.conv2d(self._pc_out, ha, pad=cp, out_mode=ops.OUT_NCHW_F32)
         return out if x.dtype == torch.float32 else out.to(x.dtype)

@@ -24,6 +24,10 @@ class GroupNorm32(nn.GroupNorm):
     def stats(self, x):
         return ops.group_norm_affine(x, self._g, self._b, self.eps, self.num_groups)
 
+    def norm(self, x, silu=True, pad=0):
+        """GroupNorm (+ SiLU) of x materialised (zero-bordered by ``pad``) — one ``sdk_group_norm``."""
+        return ops.group_norm(x, self._g, self._b, self.eps, self.num_groups, silu=silu, pad=pad)
+
     def forward(self, x):
         raise NotImplementedError("sd_amd: GroupNorm32 runs fused inside the HIP conv (use the parent block)")
 

@@ -199,7 +199,7 @@ class _Autotune:
     Enabled by ``enable()`` (UNetModel/AutoEncoderKL.prepare(autotune=True)); the
     first call of each distinct problem times every candidate (HIP events, 3 reps
     after a warm-up; SD_AMD_TUNE_REPS) and caches the fastest.  Never runs under graph capture."""
-    VARIANTS = (2, 5, 7, 6, 4, 3, 8, 9, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26)
+    VARIANTS = (2, 5, 7, 6, 4, 3, 8, 9, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 31, 32, 33)
     SPLITS = (0, 1, 2, 4, 8)
 
     def __init__(self):
@@ -236,14 +236,16 @@ class _Autotune:
             n += 1
         return n
 
-    def key(self, a, pc):
+    def key(self, a, pc, gn=False):
         s0, s1 = a.seg[0], a.seg[1]
         return (a.batch, a.ho, a.wo, a.cout, a.nseg, pc.k_total, a.out_mode, s0.cin, s0.h, s0.w, s0.ksize,
                 s0.stride, s0.upsample, s0.c_split, int(bool(s0.gn_scale) or bool(s0.silu)),
-                s1.cin if a.nseg > 1 else 0)
+                s1.cin if a.nseg > 1 else 0, int(gn))
 
-    def choose(self, a, pc, dev):
-        key = self.key(a, pc)
+    def choose(self, a, pc, dev, gn=False):
+        """``gn``: the output feeds a GroupNorm — candidates are timed emitting the statistics, and
+        plans that cannot emit them are dropped (their GroupNorm would pay a statistics pass)."""
+        key = self.key(a, pc, gn)
         hit = self.table.get(key)
         if hit is not None or not self.enabled or torch.cuda.is_current_stream_capturing():
             return hit
@@ -253,6 +255,13 @@ class _Autotune:
         best, best_t = (0, 0), float("inf")
         info = ConvPlanInfo()
         stream = _stream()
+        emit_any = False
+        if gn:                           # is there a candidate at all that emits the statistics?
+            for v in self.VARIANTS:
+                for sp in self.SPLITS:
+                    a.variant_hint, a.split_k = v + 1, sp
+                    if lib().sdk_conv2d_plan(C.byref(a), C.byref(info)) == 0 and info.gn_chunks > 0:
+                        emit_any = True
         for v in self.VARIANTS:
             for sp in self.SPLITS:
                 a.variant_hint, a.split_k = v + 1, sp
@@ -260,6 +269,14 @@ class _Autotune:
                     continue
                 if sp == 0 and info.split_k in self.SPLITS[1:]:
                     continue             # the automatic split equals an explicit candidate
+                part = None
+                if emit_any:
+                    if info.gn_chunks == 0:
+                        continue
+                    part = torch.empty(a.batch, info.gn_chunks, a.cout, 2, dtype=torch.float32, device=dev)
+                    a.gn_partial = part.data_ptr()
+                else:
+                    a.gn_partial = None
                 if info.workspace_bytes > 0:
                     ws = WORKSPACE.get(info.workspace_bytes, dev)
                     a.workspace, a.workspace_bytes = ws.data_ptr(), ws.numel()
@@ -273,7 +290,7 @@ class _Autotune:
                 t = e0.elapsed_time(e1)
                 if t < best_t:
                     best_t, best = t, (v + 1, info.split_k)
-        a.variant_hint, a.split_k = 0, 0
+        a.variant_hint, a.split_k, a.gn_partial = 0, 0, None
         self.table[key] = best
         self.timed += 1
         if self.timed % 10 == 0:             # progress (a full re-tune takes minutes)
@@ -289,14 +306,21 @@ AUTOTUNE = _Autotune()
 FORCE_VARIANT = None
 
 
+# GroupNorm statistics emitted by the producing conv (tensor attribute; see conv2d(gn_stats=True))
+GN_ATTR = "_sd_gn_partial"
+EMIT_GN_STATS = True      # tests / A/B: False = every GroupNorm runs its own statistics pass
+
+
 def conv2d(pc: PackedConv, x, *, ksize=None, stride=1, pad=None, pad_end=0, upsample=False, gn=None, silu=False,
            seg2=None, bias=True, row_bias=None, residual=None, out_mode=OUT_NHWC_F16, out=None,
-           variant=None, split_k=None, act=ACT_NONE):
+           variant=None, split_k=None, act=ACT_NONE, gn_stats=False):
     """Run the implicit-GEMM conv.  ``seg2`` = (x2, gn2, silu2) adds a fused 1x1 K segment.
     ``pad_end`` adds zero rows/cols after the source (asymmetric (0,1,0,1) padding).
     ``row_bias`` = (fp32 tensor [B, ld], column offset) — the per-(batch, channel) add.
     ``variant`` / ``split_k`` force a kernel configuration (benchmarks; default: planner
-    or autotuner)."""
+    or autotuner).  ``gn_stats``: the output feeds a GroupNorm — when the chosen plan can, the
+    epilogue also emits its per-chunk channel statistics (attached to the returned tensor,
+    consumed by ``group_norm``, which then skips its statistics pass)."""
     a = ConvArgs()
     k0 = pc.seg_geom[0][0] if ksize is None else ksize
     if pad is None:
@@ -337,7 +361,8 @@ def conv2d(pc: PackedConv, x, *, ksize=None, stride=1, pad=None, pad_end=0, upsa
         _need_cuda(residual, "conv2d residual")
         a.residual = residual.data_ptr()
         a.res_ld = residual.shape[-1]
-    tuned = AUTOTUNE.choose(a, pc, dev) if (AUTOTUNE.enabled or AUTOTUNE.table) else None
+    want_gn = gn_stats and EMIT_GN_STATS and out_mode == OUT_NHWC_F16
+    tuned = AUTOTUNE.choose(a, pc, dev, want_gn) if (AUTOTUNE.enabled or AUTOTUNE.table) else None
     if tuned is not None:
         a.variant_hint, a.split_k = tuned
     if variant is None:
@@ -352,6 +377,10 @@ def conv2d(pc: PackedConv, x, *, ksize=None, stride=1, pad=None, pad_end=0, upsa
         ws = WORKSPACE.get(info.workspace_bytes, dev)
         a.workspace = ws.data_ptr()
         a.workspace_bytes = ws.numel()
+    part = None
+    if want_gn and info.gn_chunks > 0 and out.shape[-1] == pc.N:
+        part = torch.empty(B, info.gn_chunks, pc.N, 2, dtype=torch.float32, device=dev)
+        a.gn_partial = part.data_ptr()
     if PROFILER.active:
         # algorithmic HBM bytes: each source tensor, the weights and the output once (+ residual)
         nb = sum(t.numel() * 2 for t in _as_pair(x) if t is not None) + pc.N * pc.k_total * 2
@@ -362,6 +391,8 @@ def conv2d(pc: PackedConv, x, *, ksize=None, stride=1, pad=None, pad_end=0, upsa
     check(lib().sdk_conv2d(C.byref(a), _stream()), "conv2d")
     if PROFILER.active:
         PROFILER.end()
+    if part is not None:
+        setattr(out, GN_ATTR, (part, info.gn_chunks))
     return out
 
 
@@ -497,6 +528,37 @@ def group_norm_affine(x, gamma, beta, eps, groups=32):
     if PROFILER.active:
         PROFILER.end()
     return scale, shift
+
+
+def group_norm(x, gamma, beta, eps, groups=32, silu=True, pad=0, out=None):
+    """GroupNorm (+ SiLU) end to end in one C call: statistics and apply, written contiguous or
+    zero-bordered (``pad``) for a pad-0 3x3 conv.  At the UNet's small levels one fused launch;
+    elsewhere the statistics pass then the apply pass (``sdk_group_norm``)."""
+    args, (B, H, W, Ch), dev = _gn_args(x)
+    args.groups, args.eps = groups, eps
+    args.gamma, args.beta = gamma.data_ptr(), beta.data_ptr()
+    scale = torch.empty(B, Ch, dtype=torch.float32, device=dev)
+    shift = torch.empty(B, Ch, dtype=torch.float32, device=dev)
+    args.scale, args.shift = scale.data_ptr(), shift.data_ptr()
+    ws = WORKSPACE.get(lib().sdk_group_norm_workspace(B, H * W, Ch), dev)
+    args.workspace, args.workspace_bytes = ws.data_ptr(), ws.numel()
+    y = out if out is not None else torch.empty(B, H + 2 * pad, W + 2 * pad, Ch, dtype=torch.float16, device=dev)
+    # statistics the producing convs emitted (every source must carry them)
+    srcs = [t for t in _as_pair(x) if t is not None]
+    parts = [getattr(t, GN_ATTR, None) for t in srcs]
+    p0 = p1 = None
+    n0 = n1 = 0
+    if all(pp is not None for pp in parts):
+        (p0, n0) = parts[0]
+        if len(parts) > 1:
+            (p1, n1) = parts[1]
+    if PROFILER.active:
+        PROFILER.begin("group_norm", None)
+    check(lib().sdk_group_norm(C.byref(args), 1 if silu else 0, _ptr(y), y.shape[-1], H, W, pad, _ptr(p0), n0,
+                               _ptr(p1), n1, _stream()), "group_norm")
+    if PROFILER.active:
+        PROFILER.end()
+    return y
 
 
 def layer_norm(x2d, gamma, beta, eps=1e-5, out=None):

@@ -52,10 +52,10 @@ def test_tuning_table_matches_kernel_source(bench_c3):
     missing = []
     orig = ops.AUTOTUNE.choose
 
-    def spy(a, pc, dev):
-        hit = orig(a, pc, dev)
+    def spy(a, pc, dev, gn=False):
+        hit = orig(a, pc, dev, gn)
         if hit is None:
-            missing.append(ops.AUTOTUNE.key(a, pc))
+            missing.append(ops.AUTOTUNE.key(a, pc, gn))
         return hit
     ops.AUTOTUNE.choose = spy
     try:

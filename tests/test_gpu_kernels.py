@@ -43,7 +43,7 @@ def _conv_ref(x_nhwc, w, b, stride=1, pad=1, upsample=False, gn=None, silu=False
 
 
 @pytest.fixture(params=["auto", "0", "2", "3", "4", "5", "6", "7", "8", "9", "16", "17", "18", "19", "20", "21",
-                        "22", "23", "24", "25", "26"])
+                        "22", "23", "24", "25", "26", "31", "32", "33"])
 def conv_variant(request, sdk):
     """Every conv kernel variant (register-staged 128x128, LDS-DMA 256x256/256x128/128x128)."""
     from sd_amd import ops as o
@@ -331,6 +331,111 @@ def test_group_norm_apply_concat(ops, silu):
         ref = F.silu(ref)
     assert y.shape == (B, H, W, C1 + C2)
     assert rel_l2(y, ref.permute(0, 2, 3, 1)) < 1e-3
+
+
+GLDS_VARIANTS = {2, 3, 4, 5, 6, 7, 16, 17, 18, 19, 22, 23, 24, 25, 26, 31, 32, 33}
+
+
+def _chunk_stats(y, nch):
+    """(mean, M2) per (image, chunk of hw/nch pixels, channel) of an NHWC tensor, in float64."""
+    B, H, W, C = y.shape
+    t = y.double().reshape(B, nch, H * W // nch, C)
+    mean = t.mean(2)
+    return mean, ((t - mean[:, :, None]) ** 2).sum(2)
+
+
+@pytest.mark.parametrize("H,W,Ci,Co,split", [(16, 16, 128, 320, None), (8, 8, 640, 1280, 4), (32, 32, 64, 640, None)])
+def test_conv_emits_group_norm_statistics(ops, conv_variant, H, W, Ci, Co, split):
+    """The producing conv's epilogue (or its split-K reduce) emits per-chunk channel (mean, M2) of
+    the fp16 values it stores (bias, embedding row and residual included, offset channels);
+    group_norm merges them instead of a statistics pass: same result as the pass."""
+    B = 2
+    x = _rand(B, H, W, Ci, seed=H + Ci)
+    g = torch.Generator(device="cpu").manual_seed(Co + H)
+    w = torch.randn(Co, Ci, 3, 3, generator=g) / math.sqrt(Ci * 9)
+    b = torch.randn(Co, generator=g) * 2 + 3                     # channel means far from 0
+    emb = torch.randn(B, Co + 16, generator=g)
+    res = _rand(B, H, W, Co, seed=H + Co)
+    pc = ops.PackedConv([(w, Ci)], b, device=DEV)
+    y = ops.conv2d(pc, x.to(DEV), residual=res.to(DEV), row_bias=(emb.to(DEV), 16), split_k=split, gn_stats=True)
+    ref = _conv_ref(x, w.half(), b) + emb[:, None, None, 16:] + res.float()
+    assert rel_l2(y, ref) < 3e-3
+    part = getattr(y, ops.GN_ATTR, None)
+    forced = None if conv_variant == "auto" else int(conv_variant)
+    if split or forced is None or forced in GLDS_VARIANTS:
+        assert part is not None, "this plan should emit GroupNorm statistics"
+    if part is None:
+        return
+    pp, nch = part
+    assert pp.shape == (B, nch, Co, 2) and (H * W) % nch == 0
+    mean, m2 = _chunk_stats(y, nch)
+    assert torch.allclose(pp[..., 0].double().cpu(), mean.cpu(), rtol=1e-5, atol=1e-4)
+    assert rel_l2(pp[..., 1].double().cpu(), m2.cpu()) < 1e-4
+    gamma = torch.rand(Co, generator=g).to(DEV) + 0.5
+    beta = (torch.randn(Co, generator=g) * 0.1).to(DEV)
+    g1 = ops.group_norm(y, gamma, beta, 1e-5, 32, silu=True, pad=1)
+    g0 = ops.group_norm(y.clone(), gamma, beta, 1e-5, 32, silu=True, pad=1)    # no partials: statistics pass
+    assert rel_l2(g1, g0) < 1e-3
+
+
+def test_group_norm_concat_from_partials(ops):
+    """Output-block GroupNorm over cat(h, skip): both sources carry statistics from different
+    producers (different chunkings: an M-tile epilogue and a split-K reduce)."""
+    B, H, W = 2, 16, 16
+    g = torch.Generator(device="cpu").manual_seed(5)
+    x = _rand(B, H, W, 320, seed=51).to(DEV)
+    w1 = torch.randn(640, 320, 3, 3, generator=g) / math.sqrt(320 * 9)
+    w2 = torch.randn(320, 320, 1, 1, generator=g) / math.sqrt(320)
+    pc1 = ops.PackedConv([(w1, 320)], torch.randn(640, generator=g) + 1, device=DEV)
+    pc2 = ops.PackedConv([(w2, 320)], torch.randn(320, generator=g) - 2, device=DEV)
+    h = ops.conv2d(pc1, x, split_k=2, gn_stats=True)
+    skip = ops.conv2d(pc2, x, split_k=1, gn_stats=True)
+    assert getattr(h, ops.GN_ATTR, None) is not None and getattr(skip, ops.GN_ATTR, None) is not None
+    gamma = torch.rand(960, generator=g).to(DEV) + 0.5
+    beta = (torch.randn(960, generator=g) * 0.1).to(DEV)
+    y1 = ops.group_norm((h, skip), gamma, beta, 1e-5, 32, silu=True, pad=1)
+    y0 = ops.group_norm((h.clone(), skip.clone()), gamma, beta, 1e-5, 32, silu=True, pad=1)
+    assert rel_l2(y1, y0) < 1e-3
+    ref = F.silu(F.group_norm(torch.cat([h, skip], -1).float().permute(0, 3, 1, 2), 32, gamma, beta, 1e-5))
+    ref = F.pad(ref, (1, 1, 1, 1)).permute(0, 2, 3, 1)
+    assert rel_l2(y1, ref) < 1e-3
+
+
+@pytest.mark.parametrize("H,W,C1,C2,pad,silu,offset", [
+    (32, 32, 640, 0, 1, True, 3.0),        # one-launch statistics + apply (hw <= 1024), zero-bordered
+    (16, 16, 640, 640, 1, True, -2.0),     # fused, 2-source concat (output block in_layers)
+    (8, 8, 1280, 1280, 0, False, 0.0),     # fused, contiguous, no SiLU
+    (32, 32, 960, 0, 0, True, 0.0),        # fused, 960 channels (cg = 30: 8-group slices)
+    (8, 8, 2560, 0, 1, True, 10.0),        # fused, 2560 channels (cg = 80)
+    (64, 64, 320, 0, 1, True, 3.0),        # hw = 4096: statistics pass, then the apply pass
+    (64, 64, 320, 320, 0, True, 0.0),
+    (7, 5, 64, 0, 1, True, 0.0),           # ragged image (rows not a multiple of anything)
+])
+def test_group_norm_end_to_end(ops, H, W, C1, C2, pad, silu, offset):
+    """sdk_group_norm (statistics + apply in one call; one launch at the small levels) vs F.group_norm
+    (+ SiLU) in fp32, and bitwise equal to the two-call path (affine, then apply)."""
+    B = 3
+    a = (_rand(B, H, W, C1, seed=H + C1).float() * 1.5 + offset).half()
+    b2 = _rand(B, H, W, C2, seed=H + C2 + 1) if C2 else None
+    C = C1 + C2
+    g = torch.Generator(device="cpu").manual_seed(C + H)
+    gamma, beta = torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g) * 0.1
+    src = (a.to(DEV), b2.to(DEV)) if C2 else a.to(DEV)
+    y = ops.group_norm(src, gamma.to(DEV), beta.to(DEV), 1e-5, 32, silu=silu, pad=pad)
+    assert y.shape == (B, H + 2 * pad, W + 2 * pad, C)
+    xr = (torch.cat([a, b2], -1) if C2 else a).float().permute(0, 3, 1, 2)
+    ref = F.group_norm(xr, 32, gamma, beta, 1e-5)
+    if silu:
+        ref = F.silu(ref)
+    ref = F.pad(ref, (pad, pad, pad, pad)).permute(0, 2, 3, 1)
+    assert rel_l2(y, ref) < 1e-3
+    if pad:
+        border = torch.ones(H + 2 * pad, W + 2 * pad, dtype=torch.bool)
+        border[pad:-pad, pad:-pad] = False
+        assert torch.count_nonzero(y[:, border].float()) == 0
+    two = ops.group_norm_apply(src, ops.group_norm_affine(src, gamma.to(DEV), beta.to(DEV), 1e-5), silu=silu,
+                               pad=pad)
+    assert torch.equal(y, two)
 
 
 @pytest.mark.parametrize("B,N,C,D,nk", [(2, 4096, 320, 40, 77), (2, 1024, 640, 80, 77), (1, 256, 320, 64, 77),
