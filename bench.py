@@ -461,6 +461,12 @@ def main():
                                "flops_per_launch": conv["flops"] / conv["launches"],
                                "algorithmic_bytes_per_launch": round(conv["bytes"] / conv["launches"]),
                                "traffic_unit": "bytes per launch (PMC, profiles/conv_traffic.json)"}
+            # the achievable ceilings of THIS device (random-operand MFMA loops, HBM copy; sdk_probe_*),
+            # next to the spec peak `frac` is quoted against
+            probe = ops.probe_peaks()
+            out["roofline"]["peak_measured"] = probe
+            out["roofline"]["frac_of_measured_peak"] = round(
+                ach / max(probe["mfma_16x16x32_f16_tflops"], probe["mfma_32x32x16_f16_tflops"]), 4)
         out["kernel_time_ms_profiled_step"] = {k: round(v["ms"], 2) for k, v in summ.items()}
         xa = ops.PROFILER.region_summary("cross_attention")
         if xa["launches"]:

@@ -171,6 +171,16 @@ int sdk_group_norm(const sdk_group_norm_args* a, int32_t silu, void* y, int32_t 
 int sdk_group_norm_apply_ex(const sdk_group_norm_args* a, int32_t silu, const float* post_bias, int32_t pb_ld,
                             const void* residual, int32_t res_ld, void* y, int32_t ld_y, sdk_stream_t stream);
 
+/* ---------------------------------------------------------------- device calibration probes
+ * Not on the sampling path: measure, on the box the bench runs on, the dense fp16 MFMA rate held
+ * under load (back-to-back v_mfma_f32_16x16x32_f16 (m16 = 1) or 32x32x16 on random register
+ * operands, `blocks` workgroups of 4 waves, `iters` iterations; seed = 32768 random fp16, sink =
+ * blocks*4 floats) and the HBM copy rate, next to the spec peaks the roofline is quoted against.
+ */
+double sdk_probe_mfma_flops(int32_t m16, int32_t blocks, int32_t iters);
+int sdk_probe_mfma(int32_t m16, int32_t blocks, int32_t iters, const void* seed, float* sink, sdk_stream_t stream);
+int sdk_probe_copy(const void* src, void* dst, int64_t bytes, sdk_stream_t stream);
+
 /* ---------------------------------------------------------------- LayerNorm
  * y = (x - mean) * rstd * gamma + beta over the last dim, fp16 in/out, fp32 math; gamma / beta fp32,
  * 16-byte aligned; cols a multiple of 8, <= 2048.

@@ -73,7 +73,8 @@ ACT_NONE, ACT_QUICK_GELU = 0, 1
 EXPORTS = ["sdk_conv2d_plan", "sdk_conv2d", "sdk_group_norm_workspace", "sdk_group_norm_affine", "sdk_group_norm_apply", "sdk_group_norm_apply_padded", "sdk_group_norm_apply_ex", "sdk_group_norm", "sdk_layer_norm",
            "sdk_attention", "sdk_cross_attention_block_supported", "sdk_cross_attention_block", "sdk_cross_attention_block_ln", "sdk_ddim_step", "sdk_ddpm_step", "sdk_timestep_embedding", "sdk_nchw_to_nhwc",
            "sdk_diag_gaussian_sample", "sdk_stochastic_encode", "sdk_token_embedding", "sdk_extract_patches",
-           "sdk_fold_patches", "sdk_upsample_bilinear2x", "sdk_gelu", "sdk_last_error", "sdk_version", "sdk_kernel_name"]
+           "sdk_fold_patches", "sdk_upsample_bilinear2x", "sdk_gelu", "sdk_last_error", "sdk_version", "sdk_kernel_name",
+           "sdk_probe_mfma_flops", "sdk_probe_mfma", "sdk_probe_copy"]
 
 _lib = None
 
@@ -114,6 +115,10 @@ def lib():
     L.sdk_token_embedding.argtypes = [vp, vp, vp, vp, i32, i32, i32, vp]
     L.sdk_extract_patches.argtypes = [vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp]
     L.sdk_fold_patches.argtypes = [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp]
+    L.sdk_probe_mfma_flops.argtypes = [i32, i32, i32]
+    L.sdk_probe_mfma_flops.restype = C.c_double
+    L.sdk_probe_mfma.argtypes = [i32, i32, i32, vp, vp, vp]
+    L.sdk_probe_copy.argtypes = [vp, vp, i64, vp]
     L.sdk_last_error.restype = C.c_char_p
     L.sdk_kernel_name.restype = C.c_char_p
     L.sdk_kernel_name.argtypes = [i32]

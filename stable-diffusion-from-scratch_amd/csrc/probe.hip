@@ -1,0 +1,98 @@
+// Device calibration probes (not on the sampling path): the dense fp16 MFMA rate this MI355X holds
+// under load and the HBM streaming rate, measured on the box the bench runs on, next to the spec
+// figures the roofline is quoted against (MI355X_MICROARCH.md: ~2.5 PFLOP/s dense fp16, 8 TB/s).
+//
+// MFMA: every wave keeps independent accumulators (8 of 16x16x32, 4 of 32x32x16) and issues
+// back-to-back MFMAs on random operands held in registers (the clock under load depends on operand
+// entropy, MICROARCH 'DVFS give-back'); 4-wave workgroups, the caller launches 2 per CU (2 waves per
+// SIMD).  The result is folded into `sink` so the work cannot be elided.
+// HBM: a grid-stride 16-B copy (read + write counted).
+#include <algorithm>
+
+#include "common.h"
+
+namespace sdk {
+namespace {
+
+template <bool M16>
+__global__ void __launch_bounds__(256) mfma_probe_kernel(const half_t* seed, int iters, float* sink) {
+  const int lane = threadIdx.x & 63;
+  h8 a = *reinterpret_cast<const h8*>(seed + (size_t)((blockIdx.x * 256 + threadIdx.x) & 4095) * 8);
+  h8 b = *reinterpret_cast<const h8*>(seed + (size_t)((blockIdx.x * 256 + threadIdx.x + 1777) & 4095) * 8);
+  float r = 0.f;
+  if constexpr (M16) {
+    f4 acc[8];
+    h8 bs[8];   // a distinct B operand per accumulator: eight independent chains, nothing to fold
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      acc[i] = f4{};
+      bs[i] = b;
+      bs[i][i] = (half_t)((float)b[i] + 0.25f * (float)(i + 1));
+    }
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bs[i], acc[i], 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r += (acc[i][0] + acc[i][1]) + (acc[i][2] + acc[i][3]);   // every element live
+  } else {
+    f16v acc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = f16v{};
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, acc[i], 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) r += acc[i][j];
+  }
+  if (lane == 0) sink[blockIdx.x * 4 + (threadIdx.x >> 6)] = r;
+}
+
+// 4 independent 16-B loads in flight per thread, then their stores
+__global__ void __launch_bounds__(256) copy_probe_kernel(const h8* src, h8* dst, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n; i += 4 * stride) {
+    h8 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = src[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) dst[i + u * stride] = v[u];
+  }
+  for (; i < n; i += stride) dst[i] = src[i];
+}
+
+}  // namespace
+}  // namespace sdk
+
+using namespace sdk;
+
+// FLOPs of one launch of the MFMA probe (2*M*N*K per MFMA x MFMAs per wave x waves)
+extern "C" double sdk_probe_mfma_flops(int32_t m16, int32_t blocks, int32_t iters) {
+  const double per = m16 ? 2.0 * 16 * 16 * 32 * 8 : 2.0 * 32 * 32 * 16 * 4;
+  return per * (double)iters * (double)blocks * 4.0;
+}
+
+// seed: >= 4096*8 random fp16 values; sink: >= blocks*4 floats
+extern "C" int sdk_probe_mfma(int32_t m16, int32_t blocks, int32_t iters, const void* seed, float* sink,
+                              sdk_stream_t stream) {
+  if (!seed || !sink || blocks <= 0 || iters <= 0) return fail(SDK_EINVAL, "probe_mfma: bad arguments");
+  if (m16)
+    hipLaunchKernelGGL(mfma_probe_kernel<true>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                       (const half_t*)seed, iters, sink);
+  else
+    hipLaunchKernelGGL(mfma_probe_kernel<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                       (const half_t*)seed, iters, sink);
+  return check_launch("probe_mfma");
+}
+
+extern "C" int sdk_probe_copy(const void* src, void* dst, int64_t bytes, sdk_stream_t stream) {
+  if (!src || !dst || bytes <= 0 || bytes % 16) return fail(SDK_EINVAL, "probe_copy: bad arguments");
+  const int64_t n = bytes / 16;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 256 * 16);
+  hipLaunchKernelGGL(copy_probe_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const h8*)src, (h8*)dst, n);
+  return check_launch("probe_copy");
+}

@@ -11,7 +11,10 @@ checkpoints and ``Diffusion/config.yaml`` params load unchanged.  Execution
 * the softmax(QK^T)V core is ``sdk_attention`` (flash-style, fp32 softmax);
 * to_out / FF-out / proj_out GEMMs fuse the residual add in their epilogue, the
   GEGLU projection fuses ``x * gelu(gate)`` in its epilogue;
-* the SpatialTransformer GroupNorm is applied inside the proj_in GEMM prologue.
+* the SpatialTransformer GroupNorm is one ``sdk_group_norm`` call (its statistics merged from the
+  producing conv's epilogue partials, then one apply pass) in front of the proj_in GEMM;
+* at the 320-channel (and small 640-channel) levels the cross-attention block — norm2, to_q, the
+  attention over the cached context K/V, to_out + residual, norm3 — is one kernel (xattn.hip).
 """
 from __future__ import annotations
 
@@ -50,11 +53,12 @@ def _ln_prep(ln: nn.LayerNorm, dev):
 # fused to_q + attention + to_out kernel for cross-attention on the cached context (xattn.hip),
 # routed where it measured faster than the three launches (tools/bench_xattn.py, MI355X: 320
 # channels at >= 65536 query rows — the 64x64 level at B=16: 1.07-1.11x, its CFG batch of 2 x 16:
-# 1.21x; slower at 640 channels, where one workgroup per CU is resident); SD_AMD_FUSED_XATTN=0 / 1
-# forces it off / on
+# 1.21x; 640 channels only up to 16384 rows, where one workgroup per CU is resident and larger
+# grids run two waves); SD_AMD_FUSED_XATTN=0 / 1 forces it off / on
 _FUSED_ENV = os.environ.get("SD_AMD_FUSED_XATTN")
 FUSED_CROSS_ATTENTION = _FUSED_ENV != "0"
 FUSED_XATTN_MIN_ROWS = 0 if _FUSED_ENV == "1" else 65536
+FUSED_XATTN_640_MAX_ROWS = 16384
 # norm2 / norm3 folded into that kernel (its prologue / epilogue) instead of two layer_norm launches;
 # SD_AMD_XATTN_NORMS=0 keeps the separate launches (A/B only: the bits are the same)
 FUSED_XATTN_NORMS = os.environ.get("SD_AMD_XATTN_NORMS") != "0"
@@ -63,8 +67,16 @@ FUSED_XATTN_NORMS = os.environ.get("SD_AMD_XATTN_NORMS") != "0"
 def _use_fused_xattn(channels, head_dim, nk, n_img, batch):
     if not FUSED_CROSS_ATTENTION or n_img % 64:
         return False
-    if _FUSED_ENV != "1" and (channels != 320 or batch * n_img < FUSED_XATTN_MIN_ROWS):
-        return False
+    rows = batch * n_img
+    if _FUSED_ENV != "1":
+        # measured wins (profiles/r2_xattn_fused_norms.txt, norms folded): 320 channels from 65,536 rows
+        # (1.12-1.23x); 640 channels up to 16,384 rows (1.02-1.06x; one 139 KiB group per CU, so the
+        # two-wave grids of the 640-channel CFG batches lose: 0.85-0.93x)
+        if channels == 320:
+            if rows < FUSED_XATTN_MIN_ROWS:
+                return False
+        elif channels != 640 or rows > FUSED_XATTN_640_MAX_ROWS:
+            return False
     return ops.cross_attention_block_supported(channels, head_dim, nk, n_img)
 
 

@@ -574,6 +574,46 @@ def layer_norm(x2d, gamma, beta, eps=1e-5, out=None):
     return y
 
 
+# --------------------------------------------------------------------------- device calibration
+
+def probe_peaks(reps=3):
+    """Measured dense fp16 MFMA rate (both MFMA shapes, random operands, every CU busy) and HBM copy
+    rate of this device (sdk_probe_*; HIP events, best of ``reps``) — the achievable ceilings next to
+    the spec peaks the bench's roofline is quoted against."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+    seed = torch.randn(32768, device=dev).half()
+    nsm = torch.cuda.get_device_properties(dev).multi_processor_count
+    blocks = 2 * nsm
+    sink = torch.empty(blocks * 4, dtype=torch.float32, device=dev)
+    out = {}
+    for m16, iters, name in ((1, 40000, "mfma_16x16x32_f16_tflops"), (0, 20000, "mfma_32x32x16_f16_tflops")):
+        check(lib().sdk_probe_mfma(m16, blocks, 200, _ptr(seed), _ptr(sink), _stream()), "probe_mfma")
+        best = float("inf")
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            check(lib().sdk_probe_mfma(m16, blocks, iters, _ptr(seed), _ptr(sink), _stream()), "probe_mfma")
+            e1.record()
+            e1.synchronize()
+            best = min(best, e0.elapsed_time(e1))
+        out[name] = round(lib().sdk_probe_mfma_flops(m16, blocks, iters) / (best * 1e-3) / 1e12, 1)
+    nbytes = 1 << 30
+    src = torch.empty(nbytes // 2, dtype=torch.float16, device=dev).normal_()
+    dst = torch.empty_like(src)
+    check(lib().sdk_probe_copy(_ptr(src), _ptr(dst), nbytes, _stream()), "probe_copy")
+    best = float("inf")
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        check(lib().sdk_probe_copy(_ptr(src), _ptr(dst), nbytes, _stream()), "probe_copy")
+        e1.record()
+        e1.synchronize()
+        best = min(best, e0.elapsed_time(e1))
+    out["hbm_copy_gbs"] = round(2 * nbytes / (best * 1e-3) / 1e9, 1)
+    del src, dst
+    return out
+
+
 # --------------------------------------------------------------------------- attention
 
 def attention(q, k, v, *, batch, heads, nq, nk, head_dim, scale, out=None, causal=False):

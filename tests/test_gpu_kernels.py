@@ -519,3 +519,12 @@ def test_cross_attention_block_rejects_unsupported(ops):
     assert not ops.cross_attention_block_supported(1280, 160, 77, 256)
     assert not ops.cross_attention_block_supported(320, 40, 81, 4096)
     assert not ops.cross_attention_block_supported(320, 40, 77, 100)
+
+
+def test_device_calibration_probes(ops):
+    """sdk_probe_*: the measured MFMA / HBM ceilings the bench reports beside the spec peaks are
+    plausible for an MI355X (dense fp16 <= 2.5 PFLOP/s spec, HBM <= 8 TB/s spec)."""
+    pk = ops.probe_peaks(reps=1)
+    for k in ("mfma_16x16x32_f16_tflops", "mfma_32x32x16_f16_tflops"):
+        assert 300.0 < pk[k] < 2600.0, pk
+    assert 1000.0 < pk["hbm_copy_gbs"] < 8100.0, pk

@@ -27,9 +27,12 @@ def main():
         ops.AUTOTUNE.load(tune)
     arms = [dict(kv.split("=") for kv in a.split(",")) for a in sys.argv[1:]]
     graphs = []
+    import importlib
     for arm in arms:
         for k, v in arm.items():
-            setattr(ops, k, int(v))
+            mod, _, name = k.rpartition(".")   # "attention.FUSED_XATTN_640_MAX_ROWS" -> sd_amd.openai_model.attention
+            target = importlib.import_module(f"sd_amd.openai_model.{mod}") if mod else ops
+            setattr(target, name, int(v))
         ops.AUTOTUNE.enable(True)
         unet(x, t, context=ctx)
         ops.AUTOTUNE.enable(False)
