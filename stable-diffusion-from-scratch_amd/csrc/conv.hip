@@ -81,6 +81,15 @@ __device__ __forceinline__ int swz(int row, int chunk) {   // element offset ins
 
 __device__ __forceinline__ h8 ldg16(const half_t* p) { return *reinterpret_cast<const h8*>(p); }
 
+// fp16 output row stores of the epilogues (SDK_STORE_HINT=1: non-temporal, an A/B build only)
+__device__ __forceinline__ void st_out16(half_t* p, const h8& v) {
+#if defined(SDK_STORE_HINT) && SDK_STORE_HINT == 1
+  __builtin_nontemporal_store(v, reinterpret_cast<h8*>(p));
+#else
+  *reinterpret_cast<h8*>(p) = v;
+#endif
+}
+
 // A-row context: per thread 4 rows (r = (tid>>3) + 32*i), fixed over the K loop.
 struct RowCtx {
   int b[4], oy[4], ox[4];
@@ -212,7 +221,7 @@ __device__ __forceinline__ void epilogue(const Params& p, f16v (&acc)[FM][FN], h
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] = (half_t)((float)v[q] + (float)rr[q]);
       }
-      *reinterpret_cast<h8*>(out + (size_t)m * p.out_ld + n) = v;
+      st_out16(out + (size_t)m * p.out_ld + n, v);
     }
     return;
   }
@@ -257,7 +266,7 @@ __device__ __forceinline__ void epilogue(const Params& p, f16v (&acc)[FM][FN], h
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] = (half_t)((float)v[q] + (float)rr[q]);
       }
-      *reinterpret_cast<h8*>(out + (size_t)m * p.out_ld + n) = v;
+      st_out16(out + (size_t)m * p.out_ld + n, v);
     }
     return;
   }
@@ -670,7 +679,7 @@ __device__ __forceinline__ void epilogue_lds(const Params& p, f16v (&acc)[FM][FN
 #pragma unroll
               for (int q = 0; q < 8; ++q) v[q] = (half_t)((float)v[q] + (float)rr[q]);
             }
-            *reinterpret_cast<h8*>(out + (size_t)m * p.out_ld + no) = v;
+            st_out16(out + (size_t)m * p.out_ld + no, v);
           }
         }
       }
@@ -768,7 +777,7 @@ __device__ __forceinline__ void epilogue_lds(const Params& p, f16v (&acc)[FM][FN
           for (int qq = 0; qq < 8; ++qq) v[qq] = (half_t)((float)v[qq] + (float)rcur[r][qq]);
         }
         if constexpr (GN) *reinterpret_cast<h8*>(wbuf + row * EPI_RS + c8 * 8) = v;   // final values for the stats
-        if (m < p.M && n < p.N) *reinterpret_cast<h8*>(out + (size_t)m * p.out_ld + n) = v;
+        if (m < p.M && n < p.N) st_out16(out + (size_t)m * p.out_ld + n, v);
       }
       if constexpr (GN) {   // full tiles only: every row stored
         if (nt == 2) gn_block_stats<32, 64, EPI_RS>(wbuf, gst + i * TN + jp * 32);
@@ -841,7 +850,7 @@ __device__ __forceinline__ void epi16_group(const Params& p, const f4* a, int mt
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] = (half_t)((float)v[q] + (float)rr[0][q]);
       }
-      *reinterpret_cast<h8*>(out + (size_t)m * p.out_ld + no) = v;
+      st_out16(out + (size_t)m * p.out_ld + no, v);
     }
     return;
   }
@@ -892,7 +901,7 @@ __device__ __forceinline__ void epi16_group(const Params& p, const f4* a, int mt
       for (int q = 0; q < 8; ++q) v[q] = (half_t)((float)v[q] + (float)rr[r][q]);
     }
     if constexpr (GN) *reinterpret_cast<h8*>(wbuf + row * EPG_RS + c8 * 8) = v;   // final values for the stats
-    if (m < p.M && n < p.N) *reinterpret_cast<h8*>(out + (size_t)m * p.out_ld + n) = v;
+    if (m < p.M && n < p.N) st_out16(out + (size_t)m * p.out_ld + n, v);
   }
   if constexpr (GN) gn_block_stats<16, 16 * NB, EPG_RS>(wbuf, gdst);   // full tiles only: every row stored
 }
@@ -1429,7 +1438,7 @@ __device__ __forceinline__ void epilogue16_lds(const Params& p, f4 (&acc)[4][2][
 #pragma unroll
           for (int q = 0; q < 8; ++q) v[q] = (half_t)((float)v[q] + (float)rr[q]);
         }
-        *reinterpret_cast<h8*>(out + (size_t)m * p.out_ld + no) = v;
+        st_out16(out + (size_t)m * p.out_ld + no, v);
       }
       continue;
     }
@@ -1477,7 +1486,7 @@ __device__ __forceinline__ void epilogue16_lds(const Params& p, f4 (&acc)[4][2][
 #pragma unroll
           for (int q = 0; q < 8; ++q) v[q] = (half_t)((float)v[q] + (float)rr[q]);
         }
-        *reinterpret_cast<h8*>(out + (size_t)m * p.out_ld + n) = v;
+        st_out16(out + (size_t)m * p.out_ld + n, v);
       }
     }
   }

@@ -1,8 +1,7 @@
 cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 200 --timeout-method thread -k "probes" > gpurun_out/t_p.txt 2>&1 || { tail -30 gpurun_out/t_p.txt; exit 1; }
-tail -2 gpurun_out/t_p.txt
-timeout -k 10 120 python -u -c "
-import sd_amd_loader; sd_amd_loader.load()
-from sd_amd import ops
-for i in range(3): print(ops.probe_peaks())
-" 2>&1 | grep -v amdgpu.ids
+NT=$GRAFT_REPO_ROOT/stable-diffusion-from-scratch_amd/libsdk_amd_nt.so
+for r in 1 2 3; do
+echo "default"; timeout -k 10 300 python -u tools/ab_unet.py EMIT_GN_STATS=1 2>&1 | grep UNet || exit 1
+echo "nontemporal"; SD_AMD_LIB=$NT timeout -k 10 300 python -u tools/ab_unet.py EMIT_GN_STATS=1 2>&1 | grep UNet || exit 1
+done > gpurun_out/nt_unet.txt
+cat gpurun_out/nt_unet.txt
