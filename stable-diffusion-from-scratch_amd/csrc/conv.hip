@@ -1924,6 +1924,125 @@ __global__ void __launch_bounds__(256) splitk_reduce_gn_kernel(Params p) {
   p.gnp[((size_t)b * p.gn_nch + chunk) * p.N + nn] = acc;
 }
 
+// Direct convolution for a handful of output channels (variant 34): the UNet's conv_out (320 -> 4)
+// and the VAE decoder's conv_out (128 -> 3).  The implicit GEMM pads N to a 128-wide tile (32-43x
+// wasted MFMA work) and re-reads every input pixel per tap through LDS-DMA; here a workgroup owns an
+// 8 x 32 output patch, stages its (8+2) x (32+2) input halo of one 64-channel block in LDS once, and
+// each thread accumulates its pixel's <= 8 outputs with v_dot2_f32_f16 from the halo and the
+// block's weights (LDS broadcast reads).  Input read ~1.3x once; the FMAs run on the vector ALUs.
+constexpr int DC_TX = 32, DC_LD = BK + 8;
+constexpr int DC_MAXN = 8;
+
+// TY output rows x 32 columns per workgroup; QS threads per pixel split the 64-channel block
+// (QS = 4: 2 x 32 pixels, each thread 16 channels — 4x the threads for the small UNet maps, partial
+// sums reduced through LDS; QS = 1: 8 x 32 pixels, one thread per pixel — the 512x512 VAE map)
+template <int NO, int TY, int QS>
+__global__ void __launch_bounds__(256) conv_direct_kernel(Params p) {
+  constexpr int HY = TY + 2, HX = DC_TX + 2, CPQ = BK / QS;   // halo rows / cols, channels per thread
+  static_assert(TY * DC_TX * QS == 256, "one thread per (pixel, channel split)");
+  __shared__ __attribute__((aligned(16))) half_t xs[HY * HX * DC_LD];
+  __shared__ __attribute__((aligned(16))) half_t ws[NO * 9 * BK];
+  __shared__ float red[QS > 1 ? QS * TY * DC_TX * NO : 1];
+  const Seg& g = p.seg[0];
+  const int tid = threadIdx.x;
+  const int tiles_x = (p.wo + DC_TX - 1) / DC_TX, tiles_y = (p.ho + TY - 1) / TY;
+  const int b = blockIdx.x / (tiles_x * tiles_y), t = blockIdx.x - b * tiles_x * tiles_y;
+  const int oy0 = (t / tiles_x) * TY, ox0 = (t % tiles_x) * DC_TX;
+  const int pix = tid % (TY * DC_TX), q = tid / (TY * DC_TX);
+  const int ty = pix / DC_TX, tx = pix % DC_TX;
+  // halo origin: input (oy0 - org, ox0 - org); 3x3 taps read halo (ty + ky, tx + kx), a 1x1 reads its centre
+  const int ks = g.ksize, org = ks == 3 ? g.pad : 1, off = ks == 3 ? 0 : 1;
+  float acc[NO];
+#pragma unroll
+  for (int o = 0; o < NO; ++o) acc[o] = 0.f;
+  const int nblk = g.cin_pad / BK;
+  for (int cb = 0; cb < nblk; ++cb) {
+    // halo: HY x HX pixels x 64 channels, 16-B vectors; zeros outside the image (pad) and past cin
+    for (int e = tid; e < HY * HX * (BK / 8); e += 256) {
+      const int px = e / (BK / 8), v = e - px * (BK / 8);
+      const int hy = px / HX, hx = px - hy * HX;
+      const int iy = oy0 - org + hy, ix = ox0 - org + hx;
+      const int c = cb * BK + v * 8;
+      h8 val = {};
+      if ((unsigned)iy < (unsigned)g.h && (unsigned)ix < (unsigned)g.w && c < g.cin)
+        val = *reinterpret_cast<const h8*>(g.src0 + ((size_t)(b * g.h + iy) * g.w + ix) * g.ld0 + c);
+      *reinterpret_cast<h8*>(xs + px * DC_LD + v * 8) = val;
+    }
+    // weights of the block: packed row n, columns (cb * taps + tap) * 64 + j
+    for (int e = tid; e < NO * ks * ks * (BK / 8); e += 256) {
+      const int n = e / (ks * ks * (BK / 8)), r = e - n * (ks * ks * (BK / 8));
+      const int tap = r / (BK / 8), v = r - tap * (BK / 8);
+      h8 wv = {};
+      if (n < p.N) wv = *reinterpret_cast<const h8*>(p.W + (size_t)n * p.ldw + (size_t)(cb * ks * ks + tap) * BK + v * 8);
+      *reinterpret_cast<h8*>(ws + (n * 9 + tap) * BK + v * 8) = wv;
+    }
+    __syncthreads();
+    for (int tap = 0; tap < ks * ks; ++tap) {
+      const int dy = tap / ks + off, dx = tap % ks + off;
+      const half_t* xr = xs + ((ty + dy) * HX + tx + dx) * DC_LD + q * CPQ;
+#pragma unroll
+      for (int v = 0; v < CPQ / 8; ++v) {
+        const h8 xv = *reinterpret_cast<const h8*>(xr + v * 8);
+#pragma unroll
+        for (int o = 0; o < NO; ++o) {
+          const h8 wv = *reinterpret_cast<const h8*>(ws + (o * 9 + tap) * BK + q * CPQ + v * 8);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const h2 xa = {xv[2 * j], xv[2 * j + 1]}, wa = {wv[2 * j], wv[2 * j + 1]};
+            acc[o] = __builtin_amdgcn_fdot2(xa, wa, acc[o], false);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if constexpr (QS > 1) {
+#pragma unroll
+    for (int o = 0; o < NO; ++o) red[(q * TY * DC_TX + pix) * NO + o] = acc[o];
+    __syncthreads();
+    if (q != 0) return;
+#pragma unroll
+    for (int o = 0; o < NO; ++o) {
+      float a = acc[o];
+#pragma unroll
+      for (int k = 1; k < QS; ++k) a += red[(k * TY * DC_TX + pix) * NO + o];
+      acc[o] = a;
+    }
+  }
+  const int oy = oy0 + ty, ox = ox0 + tx;
+  if (oy >= p.ho || ox >= p.wo) return;
+  const int m = (b * p.ho + oy) * p.wo + ox;
+#pragma unroll
+  for (int o = 0; o < NO; ++o) {
+    if (o >= p.N) break;
+    const float val = acc[o] + (p.bias ? p.bias[o] : 0.f);
+    if (p.out_mode == SDK_OUT_NCHW_F32)
+      reinterpret_cast<float*>(p.out)[((size_t)b * p.N + o) * p.hw_out + oy * p.wo + ox] = val;
+    else if (p.out_mode == SDK_OUT_ROWS_F32)
+      reinterpret_cast<float*>(p.out)[(size_t)m * p.out_ld + o] = val;
+    else
+      reinterpret_cast<half_t*>(p.out)[(size_t)m * p.out_ld + o] = (half_t)val;
+  }
+}
+
+// pixel tiles: 8 x 32 with one thread per pixel when that already fills the chip (>= 4 workgroups
+// per CU), else 2 x 32 with four channel splits per pixel
+template <int NO>
+int launch_direct_n(const Params& p, hipStream_t s) {
+  const int big = ((p.wo + DC_TX - 1) / DC_TX) * ((p.ho + 7) / 8) * p.batch;
+  if (big >= 1024) {
+    hipLaunchKernelGGL((conv_direct_kernel<NO, 8, 1>), dim3(big), dim3(256), 0, s, p);
+  } else {
+    const int small = ((p.wo + DC_TX - 1) / DC_TX) * ((p.ho + 1) / 2) * p.batch;
+    hipLaunchKernelGGL((conv_direct_kernel<NO, 2, 4>), dim3(small), dim3(256), 0, s, p);
+  }
+  return check_launch("conv_direct");
+}
+
+int launch_direct(const Params& p, hipStream_t s) {
+  return p.N <= 4 ? launch_direct_n<4>(p, s) : launch_direct_n<8>(p, s);
+}
+
 template <class CF>
 int launch_glds(const Params& p, hipStream_t s) {
   static std::atomic<unsigned long long> attr_set{0};   // per device: the dynamic-LDS cap is raised once
@@ -2063,16 +2182,42 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   // forced configuration: the caller's autotuner (variant_hint = 1 + id) or, for
   // benchmarks, SDK_CONV_VARIANT=id (read once, at library load)
   const int forced = a->variant_hint > 0 ? a->variant_hint - 1 : g_env_variant;
+  // variant 34: direct convolution for <= 8 output channels (conv_out of the UNet / VAE decoder)
+  {
+    const sdk_conv_src& g = a->seg[0];
+    const bool direct_ok = a->nseg == 1 && a->cout <= DC_MAXN && (g.ksize == 3 || (g.ksize == 1 && g.pad == 0)) &&
+                           g.stride == 1 && !g.upsample && g.pad_end == 0 && g.pad <= 1 && g.c_split == g.cin &&
+                           g.gn_scale == nullptr && !g.silu && !a->residual && !a->row_bias &&
+                           a->act == SDK_ACT_NONE && a->out_mode != SDK_OUT_GEGLU_F16;
+    if (forced == 34 && !direct_ok) return fail(SDK_EINVAL, "conv2d: variant 34 (direct) does not fit this conv");
+    if (direct_ok && (forced < 0 || forced == 34)) {
+      p.variant = 34;
+      p.split = 1;
+      p.tiles_m = p.tiles_n = 1;
+      p.Npad = p.N;
+      p.kt_per_split = kt;
+      if (info) {
+        info->split_k = 1;
+        info->grid_tiles = ((a->wo + DC_TX - 1) / DC_TX) * ((a->ho + 7) / 8) * a->batch;
+        info->workspace_bytes = 0;
+        info->variant = 34;
+        info->flops = 2.0 * p.M * (double)p.N * kreal;
+        info->gn_chunks = 0;
+      }
+      if (a->gn_partial) return fail(SDK_EINVAL, "conv2d: the direct variant emits no GroupNorm statistics");
+      return SDK_OK;
+    }
+  }
   // ids: 0 register-staged; 2..7 LDS-DMA configs; 8, 9 phased 256x256; 10..15 diagnostics;
   // 16..19 deep-ring LDS-DMA configs; 20, 21 phased 256x256 on v_mfma_f32_16x16x32_f16;
   // 22..26 LDS-DMA configs 5, 7, 6, 19, 18 on v_mfma_f32_16x16x32_f16; 27..30 diagnostics;
-  // 31, 32 two-per-CU 128x160 / 128x128 (16x16x32); 33 128x160 with a 4-stage ring.
+  // 31, 32 two-per-CU 128x160 / 128x128 (16x16x32); 33 128x160 with a 4-stage ring; 34 direct (<= 8 outputs).
   // The diagnostic ablations compute wrong outputs by design: the product library rejects them,
   // only the separate diagnostics build (-DSDK_CONV_DIAGNOSTICS, libsdk_amd_diag.so) runs them.
   if (is_diagnostic_variant(forced) && !kDiagnostics)
     return fail(SDK_EINVAL, "conv2d: variant " + std::to_string(forced) +
                                 " is a diagnostic ablation (only in libsdk_amd_diag.so)");
-  if (forced > 33 || forced == 1) return fail(SDK_EINVAL, "conv2d: unknown variant " + std::to_string(forced));
+  if (forced > 34 || forced == 1) return fail(SDK_EINVAL, "conv2d: unknown variant " + std::to_string(forced));
   const int fbase = forced;
   const bool fvalid = forced >= 0 && forced != 1 && forced <= 33;
   const bool fgeglu = (fbase <= 4 || fbase >= 8) && fbase != 22 && fbase != 23 && fbase != 24 && fbase != 31 &&
@@ -2189,6 +2334,7 @@ extern "C" int sdk_conv2d(const sdk_conv_args* a, sdk_stream_t stream) {
     case 31: rc = launch_glds<Cfg128x160o2m>(p, s); break;
     case 32: rc = launch_glds<Cfg128x128o2m>(p, s); break;
     case 33: rc = launch_glds<Cfg128x160r4m>(p, s); break;
+    case 34: rc = launch_direct(p, s); break;
 #ifdef SDK_CONV_DIAGNOSTICS
     case 27: rc = launch_ph<PhCfg8, 128>(p, s); break;   // diagnostics: no W DMA issued
     case 28: rc = launch_ph<PhCfg8, 256>(p, s); break;   // diagnostics: no A DMA issued

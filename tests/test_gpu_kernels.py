@@ -528,3 +528,31 @@ def test_device_calibration_probes(ops):
     for k in ("mfma_16x16x32_f16_tflops", "mfma_32x32x16_f16_tflops"):
         assert 300.0 < pk[k] < 2600.0, pk
     assert 1000.0 < pk["hbm_copy_gbs"] < 8100.0, pk
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout,k,pad,mode", [
+    (2, 16, 16, 320, 4, 3, 1, "nchw"),      # UNet conv_out (masked halo)
+    (2, 18, 18, 320, 4, 3, 0, "nchw"),      # UNet conv_out on the zero-bordered GN output
+    (1, 34, 66, 128, 3, 3, 0, "nchw"),      # VAE conv_out shape (ragged 8x32 patches)
+    (3, 9, 40, 64, 8, 3, 1, "nhwc"),        # fp16 NHWC out, 8 outputs
+    (2, 12, 12, 192, 5, 1, 0, "rows"),      # 1x1, fp32 rows
+])
+def test_conv_direct_small_n(ops, B, H, W, Cin, Cout, k, pad, mode):
+    """Variant 34 (direct convolution for <= 8 outputs: halo tile in LDS, v_dot2_f32_f16) vs fp32
+    torch; the planner picks it by itself for these shapes."""
+    x = _rand(B, H, W, Cin, seed=H + Cin)
+    w = torch.randn(Cout, Cin, k, k) / math.sqrt(Cin * k * k)
+    b = torch.randn(Cout) * 0.1
+    pc = ops.PackedConv([(w, Cin)], b, device=DEV)
+    om = {"nchw": ops.OUT_NCHW_F32, "nhwc": ops.OUT_NHWC_F16, "rows": ops.OUT_ROWS_F32}[mode]
+    y = ops.conv2d(pc, x.to(DEV), pad=pad, out_mode=om)
+    y34 = ops.conv2d(pc, x.to(DEV), pad=pad, out_mode=om, variant=34)
+    assert torch.equal(y, y34), "the planner must pick the direct variant for <= 8 outputs"
+    ref = _conv_ref(x, w.half(), b, pad=pad)
+    if mode == "nchw":
+        ref = ref.permute(0, 3, 1, 2)
+    assert y.shape == ref.shape
+    assert rel_l2(y, ref) < 2e-3
+    with pytest.raises(RuntimeError):                      # does not fit: a 2-source concat
+        ops.conv2d(pc, (x.to(DEV)[..., :Cin // 2].contiguous(), x.to(DEV)[..., Cin // 2:].contiguous()),
+                   pad=pad, out_mode=om, variant=34)
