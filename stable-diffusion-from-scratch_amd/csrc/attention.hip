@@ -175,6 +175,12 @@ __global__ void __launch_bounds__(NW * 64, QB == 2 ? 1 : 2) attn_fwd_kernel(Attn
   stage(0);
   if (ntiles > 1) fetch(1);
   __syncthreads();
+#if !defined(SDK_NO_PRIO)
+  // static priority for the second-dispatched half of an 8-wave group (it otherwise loses VALU
+  // arbitration to its SIMD partner every tile, MI355X_MICROARCH.md two-waves item 4; UNet step
+  // -0.2 %, profiles/r2_static_priority_ab.txt)
+  if (NW == 8 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+#endif
 
   for (int t = 0; t < ntiles; ++t) {
     const int cur = t & 1;

@@ -1282,6 +1282,12 @@ __global__ void __launch_bounds__(CF::NT, CF::OCC * CF::NW / 4) conv_glds_kernel
 #pragma unroll
   for (int s = 0; s < CF::NS - 1; ++s) SDK_STAGE(kt0 + s, s);
   int buf = 0, wbuf = CF::NS - 1;
+#if !defined(SDK_NO_PRIO)
+  // static priority for the younger half of the workgroup's waves (the arbitration loser on every
+  // K-step otherwise; UNet step -0.4 %, profiles/r2_static_priority_ab.txt — priority flips around
+  // each K-step's MFMA cluster measured +0.2 %)
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= CF::NT / 2) __builtin_amdgcn_s_setprio(1);
+#endif
   for (int kt = kt0; kt < kt1; ++kt) {
     SDK_STAGE(kt + CF::NS - 1, wbuf);
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"((CF::NS - 1) * GPW) : "memory");
