@@ -392,7 +392,9 @@ def conv2d(pc: PackedConv, x, *, ksize=None, stride=1, pad=None, pad_end=0, upsa
     if PROFILER.active:
         PROFILER.end()
     if part is not None:
-        setattr(out, GN_ATTR, (part, info.gn_chunks))
+        # the statistics describe `out` as written now: group_norm ignores them once the tensor has
+        # been modified in place (its version counter moved)
+        setattr(out, GN_ATTR, (part, info.gn_chunks, out._version))
     return out
 
 
@@ -546,12 +548,13 @@ def group_norm(x, gamma, beta, eps, groups=32, silu=True, pad=0, out=None):
     # statistics the producing convs emitted (every source must carry them)
     srcs = [t for t in _as_pair(x) if t is not None]
     parts = [getattr(t, GN_ATTR, None) for t in srcs]
+    parts = [pp if pp is not None and pp[2] == t._version else None for pp, t in zip(parts, srcs)]
     p0 = p1 = None
     n0 = n1 = 0
     if all(pp is not None for pp in parts):
-        (p0, n0) = parts[0]
+        (p0, n0, _) = parts[0]
         if len(parts) > 1:
-            (p1, n1) = parts[1]
+            (p1, n1, _) = parts[1]
     if PROFILER.active:
         PROFILER.begin("group_norm", None)
     check(lib().sdk_group_norm(C.byref(args), 1 if silu else 0, _ptr(y), y.shape[-1], H, W, pad, _ptr(p0), n0,

@@ -366,7 +366,7 @@ def test_conv_emits_group_norm_statistics(ops, conv_variant, H, W, Ci, Co, split
         assert part is not None, "this plan should emit GroupNorm statistics"
     if part is None:
         return
-    pp, nch = part
+    pp, nch, _ = part
     assert pp.shape == (B, nch, Co, 2) and (H * W) % nch == 0
     mean, m2 = _chunk_stats(y, nch)
     assert torch.allclose(pp[..., 0].double().cpu(), mean.cpu(), rtol=1e-5, atol=1e-4)
@@ -376,6 +376,11 @@ def test_conv_emits_group_norm_statistics(ops, conv_variant, H, W, Ci, Co, split
     g1 = ops.group_norm(y, gamma, beta, 1e-5, 32, silu=True, pad=1)
     g0 = ops.group_norm(y.clone(), gamma, beta, 1e-5, 32, silu=True, pad=1)    # no partials: statistics pass
     assert rel_l2(g1, g0) < 1e-3
+    # modified in place after the conv: the emitted statistics are stale and must not be used
+    y.mul_(2.0).add_(1.0)
+    g2 = ops.group_norm(y, gamma, beta, 1e-5, 32, silu=True, pad=1)
+    g3 = ops.group_norm(y.clone(), gamma, beta, 1e-5, 32, silu=True, pad=1)
+    assert torch.equal(g2, g3)
 
 
 def test_group_norm_concat_from_partials(ops):
