@@ -2049,6 +2049,88 @@ int launch_direct(const Params& p, hipStream_t s) {
   return p.N <= 4 ? launch_direct_n<4>(p, s) : launch_direct_n<8>(p, s);
 }
 
+// Skinny GEMM for M <= 64 rows (variant 35): the time-embedding MLP and the ResBlock embedding
+// projections run at M = batch (16 at the bench), where a 128-row tile wastes 7/8 of its MFMA work
+// and the 1280 x 20160 weight is streamed by a few dozen workgroups (~30 us per launch).  Here a
+// workgroup owns 16 output columns and its 4 waves split K; each lane streams 16-B pieces of its
+// column's packed weight row straight from HBM (every weight byte is read once, SK_PF K-steps in
+// flight), the A fragments (x rows, SiLU applied on load) come from L2, v_mfma_f32_16x16x32_f16
+// accumulates M/16 row blocks per weight fragment, and the 4 wave partials are summed through LDS.
+// 16x16x32 operand layout: lane l supplies A[row l%16][k 8(l/16)..+8] and B[k 8(l/16)..+8][col l%16];
+// D element i of lane l is D[4(l/16) + i][l%16].
+constexpr int SK_MAXM = 64, SK_PF = 8;
+
+template <int MB>   // 16-row blocks
+__global__ void __launch_bounds__(256) conv_skinny_kernel(Params p) {
+  __shared__ float red[4][MB][4][64];
+  const Seg& g = p.seg[0];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.x * 16, K = g.cin;
+  const int ksteps = (K + 31) / 32, per = (ksteps + 3) / 4;
+  const int kb = min(ksteps, wave * per), ke = min(ksteps, kb + per);
+  const int kl = (lane >> 4) * 8;
+  const half_t* wrow = p.W + (size_t)(n0 + (lane & 15)) * p.ldw;   // rows < wrows (N padded to 128)
+  f4 acc[MB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) acc[mb] = f4{};
+  for (int k0 = kb; k0 < ke; k0 += SK_PF) {
+    h8 w[SK_PF];
+#pragma unroll
+    for (int u = 0; u < SK_PF; ++u) {
+      const int k = (k0 + u) * 32 + kl;
+      w[u] = (k0 + u < ke && k < K) ? ldg16(wrow + k) : h8{};
+    }
+#pragma unroll
+    for (int u = 0; u < SK_PF; ++u) {
+      if (k0 + u >= ke) break;
+      const int k = (k0 + u) * 32 + kl;
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) {
+        const int row = mb * 16 + (lane & 15);
+        h8 a = {};
+        if (row < p.M && k < K) {
+          a = ldg16(g.src0 + (size_t)row * g.ld0 + k);
+          if (g.silu) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const float x = (float)a[j];
+              a[j] = (half_t)(x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)));
+            }
+          }
+        }
+        acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, w[u], acc[mb], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[wave][mb][i][lane] = acc[mb][i];
+  __syncthreads();
+  for (int e = tid; e < MB * 4 * 64; e += 256) {
+    const int mb = e / 256, i = (e >> 6) & 3, l = e & 63;
+    const int row = mb * 16 + 4 * (l >> 4) + i, n = n0 + (l & 15);
+    if (row >= p.M || n >= p.N) continue;
+    float v = red[0][mb][i][l] + red[1][mb][i][l] + red[2][mb][i][l] + red[3][mb][i][l];
+    if (p.bias) v += p.bias[n];
+    if (p.row_bias) v += p.row_bias[(size_t)(row / p.hw_out) * p.rb_ld + n];
+    v = act_fn(p.act, v);
+    if (p.res) v += (float)p.res[(size_t)row * p.res_ld + n];
+    if (p.out_mode == SDK_OUT_ROWS_F32)
+      reinterpret_cast<float*>(p.out)[(size_t)row * p.out_ld + n] = v;
+    else
+      reinterpret_cast<half_t*>(p.out)[(size_t)row * p.out_ld + n] = (half_t)v;
+  }
+}
+
+int launch_skinny(const Params& p, hipStream_t s) {
+  const dim3 grid((p.N + 15) / 16);
+  if (p.M <= 16) hipLaunchKernelGGL(conv_skinny_kernel<1>, grid, dim3(256), 0, s, p);
+  else if (p.M <= 32) hipLaunchKernelGGL(conv_skinny_kernel<2>, grid, dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(conv_skinny_kernel<4>, grid, dim3(256), 0, s, p);
+  return check_launch("conv_skinny");
+}
+
 template <class CF>
 int launch_glds(const Params& p, hipStream_t s) {
   static std::atomic<unsigned long long> attr_set{0};   // per device: the dynamic-LDS cap is raised once
@@ -2214,6 +2296,31 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
       return SDK_OK;
     }
   }
+  // variant 35: skinny GEMM for <= 64 rows (token GEMMs at M = batch: the time-embedding MLP)
+  {
+    const sdk_conv_src& g = a->seg[0];
+    const bool skinny_ok = a->nseg == 1 && p.M <= SK_MAXM && g.ksize == 1 && g.stride == 1 && g.pad == 0 &&
+                           g.pad_end == 0 && !g.upsample && g.c_split == g.cin && g.gn_scale == nullptr &&
+                           (a->out_mode == SDK_OUT_NHWC_F16 || a->out_mode == SDK_OUT_ROWS_F32) && !a->gn_partial;
+    if (forced == 35 && !skinny_ok) return fail(SDK_EINVAL, "conv2d: variant 35 (skinny) does not fit this GEMM");
+    if (skinny_ok && (forced < 0 || forced == 35)) {
+      p.variant = 35;
+      p.split = 1;
+      p.tiles_m = 1;
+      p.tiles_n = (p.N + 15) / 16;
+      p.Npad = p.N;
+      p.kt_per_split = kt;
+      if (info) {
+        info->split_k = 1;
+        info->grid_tiles = p.tiles_n;
+        info->workspace_bytes = 0;
+        info->variant = 35;
+        info->flops = 2.0 * p.M * (double)p.N * kreal;
+        info->gn_chunks = 0;
+      }
+      return SDK_OK;
+    }
+  }
   // ids: 0 register-staged; 2..7 LDS-DMA configs; 8, 9 phased 256x256; 10..15 diagnostics;
   // 16..19 deep-ring LDS-DMA configs; 20, 21 phased 256x256 on v_mfma_f32_16x16x32_f16;
   // 22..26 LDS-DMA configs 5, 7, 6, 19, 18 on v_mfma_f32_16x16x32_f16; 27..30 diagnostics;
@@ -2223,7 +2330,7 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   if (is_diagnostic_variant(forced) && !kDiagnostics)
     return fail(SDK_EINVAL, "conv2d: variant " + std::to_string(forced) +
                                 " is a diagnostic ablation (only in libsdk_amd_diag.so)");
-  if (forced > 34 || forced == 1) return fail(SDK_EINVAL, "conv2d: unknown variant " + std::to_string(forced));
+  if (forced > 35 || forced == 1) return fail(SDK_EINVAL, "conv2d: unknown variant " + std::to_string(forced));
   const int fbase = forced;
   const bool fvalid = forced >= 0 && forced != 1 && forced <= 33;
   const bool fgeglu = (fbase <= 4 || fbase >= 8) && fbase != 22 && fbase != 23 && fbase != 24 && fbase != 31 &&
@@ -2341,6 +2448,7 @@ extern "C" int sdk_conv2d(const sdk_conv_args* a, sdk_stream_t stream) {
     case 32: rc = launch_glds<Cfg128x128o2m>(p, s); break;
     case 33: rc = launch_glds<Cfg128x160r4m>(p, s); break;
     case 34: rc = launch_direct(p, s); break;
+    case 35: rc = launch_skinny(p, s); break;
 #ifdef SDK_CONV_DIAGNOSTICS
     case 27: rc = launch_ph<PhCfg8, 128>(p, s); break;   // diagnostics: no W DMA issued
     case 28: rc = launch_ph<PhCfg8, 256>(p, s); break;   // diagnostics: no A DMA issued

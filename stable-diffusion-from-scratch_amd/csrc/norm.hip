@@ -389,6 +389,127 @@ __global__ void __launch_bounds__(256) gn_finalize_part_kernel(const float2* par
   }
 }
 
+// GroupNorm apply whose prologue merges the producers' partials itself (one launch instead of
+// gn_finalize_part + apply: at the 32x32 / 16x16 / 8x8 levels both are latency-floor launches).
+// grid (groups / gps channel slices, batch, row splits of the output image): a workgroup Chan-merges
+// its slice's channels over the partial chunks (double, chunk order), merges the slice's groups from
+// the channels exactly as gn_finalize_part_kernel does, keeps scale / shift in LDS and normalises
+// (+ SiLU) its rows of the (optionally zero-bordered) image for the slice's channels.  The partials
+// are read once per workgroup from L2 (nch x slice x 8 B), so the path is taken only for hw up to
+// SDK_GN_PART_FUSED_MAX_HW (default 256: the 16x16 / 8x8 levels, 7.6 vs 9.8 us per GroupNorm at 8x8;
+// at 32x32 the per-workgroup prologue repeats over too many row splits: 16-17 vs 15.4 us, measured
+// same-box, UNet step 21.07 -> 21.01 ms at 256 and 21.10 at 1024).
+constexpr int GNP_MAXCS = 256, GNP_MAXCH = 16;   // slice channels, partial chunks per source
+
+__global__ void __launch_bounds__(256) gn_apply_part_kernel(const float2* part0, int nch0, const float2* part1,
+                                                            int nch1, const half_t* s0, const half_t* s1, int c_split,
+                                                            int ld0, int ld1, int h, int w, int pad, int channels,
+                                                            int cg, int gps, float eps, const float* gamma,
+                                                            const float* beta, float* scale, float* shift, int silu,
+                                                            half_t* y, int ldy, int rows_per) {
+  __shared__ double cm[GNP_MAXCS], cq[GNP_MAXCS];
+  __shared__ float sc_s[GNP_MAXCS], sh_s[GNP_MAXCS];
+  __shared__ float2 stage[GNP_MAXCH * GNP_MAXCS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cs = gps * cg, c0 = blockIdx.x * cs, b = blockIdx.y;
+  const int hw = h * w;
+  // all of the slice's partials into LDS at once (independent, coalesced loads), then the merges
+  const int nchm = max(nch0, part1 ? nch1 : 0);
+  for (int e = tid; e < nchm * cs; e += 256) {
+    const int k = e / cs, cc = e - k * cs, c = c0 + cc;
+    const bool second = c >= c_split;
+    const int nch = second ? nch1 : nch0, csz = second ? channels - c_split : c_split, cl = second ? c - c_split : c;
+    if (k < nch) stage[k * cs + cc] = (second ? part1 : part0)[((size_t)b * nch + k) * csz + cl];
+  }
+  __syncthreads();
+  // equal-count chunks: mean = mean of the chunk means, M2 = sum M2_k + rows * sum (mean_k - mean)^2
+  for (int cc = tid; cc < cs; cc += 256) {
+    const int c = c0 + cc;
+    const int nch = c >= c_split ? nch1 : nch0;
+    double ms = 0.0;
+    for (int k = 0; k < nch; ++k) ms += (double)stage[k * cs + cc].x;
+    const double mean = ms / nch, rows = (double)hw / nch;
+    double m2 = 0.0, dd = 0.0;
+    for (int k = 0; k < nch; ++k) {
+      const float2 q = stage[k * cs + cc];
+      const double dl = (double)q.x - mean;
+      m2 += (double)q.y;
+      dd += dl * dl;
+    }
+    cm[cc] = mean;
+    cq[cc] = m2 + rows * dd;
+  }
+  __syncthreads();
+  for (int gi = wave; gi < gps; gi += 4) {
+    double ms = 0.0;
+    for (int ci = lane; ci < cg; ci += 64) ms += cm[gi * cg + ci];
+    ms = wave_sum_d(ms);
+    const double mg = ms / cg;
+    double m2g = 0.0;
+    for (int ci = lane; ci < cg; ci += 64) {
+      const double dm = cm[gi * cg + ci] - mg;
+      m2g += cq[gi * cg + ci] + (double)hw * dm * dm;
+    }
+    m2g = wave_sum_d(m2g);
+    const double var = (m2g > 0 ? m2g : 0.0) / ((double)hw * cg);
+    const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+    const float meanf = (float)mg;
+    for (int ci = lane; ci < cg; ci += 64) {
+      const int c = c0 + gi * cg + ci;
+      const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+      const float sc = gm * rstd, sh = bt - meanf * sc;
+      sc_s[gi * cg + ci] = sc;
+      sh_s[gi * cg + ci] = sh;
+      if (scale && blockIdx.z == 0) {
+        scale[(size_t)b * channels + c] = sc;
+        shift[(size_t)b * channels + c] = sh;
+      }
+    }
+  }
+  __syncthreads();
+  const int hp = h + 2 * pad, wp = w + 2 * pad, npix = hp * wp, v8 = cs / 8;
+  const int r0 = blockIdx.z * rows_per, r1 = min(npix, r0 + rows_per);
+  half_t* yb = y + (size_t)b * npix * ldy + c0;
+  constexpr int U = 8;   // vectors per thread in flight (the loads of one round are independent)
+  const int total = (r1 - r0) * v8;
+  for (int base = tid; base < total; base += 256 * U) {
+    h8 v[U];
+    bool in[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = base + u * 256, rr = r0 + e / v8, cv = (e % v8) * 8;
+      const int iy = rr / wp - pad, ix = rr % wp - pad;
+      in[u] = e < total && (unsigned)iy < (unsigned)h && (unsigned)ix < (unsigned)w;
+      v[u] = in[u] ? load_px(s0, s1, c_split, ld0, ld1, ((size_t)b * h + iy) * w + ix, c0 + cv) : h8{};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = base + u * 256, rr = r0 + e / v8, cv = (e % v8) * 8;
+      if (e >= total) break;
+      h8 o = {};
+      if (in[u]) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float x = (float)v[u][j] * sc_s[cv + j] + sh_s[cv + j];
+          if (silu) x = x * __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+          o[j] = (half_t)x;
+        }
+      }
+      *reinterpret_cast<h8*>(yb + (size_t)rr * ldy + cv) = o;
+    }
+  }
+}
+
+// channel slice of gn_apply_part_kernel: the most whole groups with a multiple of 8 channels, at most
+// GNP_MAXCS (wider per-pixel runs coalesce better); 0 = not applicable
+int gn_part_gps(int channels, int groups) {
+  const int cg = channels / groups;
+  int best = 0;
+  for (int g = 1; g <= groups; ++g)
+    if (groups % g == 0 && (g * cg) % 8 == 0 && g * cg <= GNP_MAXCS) best = g;
+  return best;
+}
+
 // slice size of the single-launch statistics: the fewest whole groups whose channels are a
 // multiple of 8 (16-B loads), at most 512 channels; 0 = not applicable
 int gn_fused_gps(int channels, int groups) {
@@ -728,6 +849,11 @@ static const int g_gn_apply_fused_max_hw = [] {
   const char* e = getenv("SDK_GN_APPLY_FUSED_MAX_HW");
   return e ? atoi(e) : 64;
 }();
+// largest image (h*w) whose GroupNorm-from-partials runs as one gn_apply_part_kernel launch
+static const int g_gn_part_fused_max_hw = [] {
+  const char* e = getenv("SDK_GN_PART_FUSED_MAX_HW");
+  return e ? atoi(e) : 256;
+}();
 
 extern "C" int sdk_group_norm(const sdk_group_norm_args* a, int32_t silu, void* y, int32_t ld_y, int32_t h, int32_t w,
                               int32_t pad, const float* part0, int32_t nch0, const float* part1, int32_t nch1,
@@ -753,6 +879,23 @@ extern "C" int sdk_group_norm(const sdk_group_norm_args* a, int32_t silu, void* 
                        a->channels / a->groups, gps, a->eps, a->gamma, a->beta, nullptr, nullptr, silu, (half_t*)y,
                        ld_y, h, w, pad);
     return check_launch("gn_fused_apply");
+  }
+  const int pgps = gn_part_gps(a->channels, a->groups);
+  if (parts && pgps > 0 && a->hw <= g_gn_part_fused_max_hw && a->batch > 0 && nch0 <= GNP_MAXCH &&
+      (!concat || nch1 <= GNP_MAXCH)) {
+    const int cs = pgps * (a->channels / a->groups), slices = a->groups / pgps;
+    const int npix = (h + 2 * pad) * (w + 2 * pad);
+    // ~8 vectors per thread (one round of loads in flight), at least ~512 workgroups when the image allows
+    int splits = std::max(1, (npix * (cs / 8) + 2047) / 2048);
+    const int want = (512 + slices * a->batch - 1) / (slices * a->batch);
+    splits = std::min(std::max(splits, want), std::max(1, npix / 16));
+    const int rows_per = (npix + splits - 1) / splits;
+    splits = (npix + rows_per - 1) / rows_per;
+    hipLaunchKernelGGL(gn_apply_part_kernel, dim3(slices, a->batch, splits), dim3(256), 0, s, (const float2*)part0,
+                       nch0, (const float2*)part1, nch1, (const half_t*)a->src0, (const half_t*)a->src1, a->c_split,
+                       a->ld0, a->ld1, h, w, pad, a->channels, a->channels / a->groups, pgps, a->eps, a->gamma,
+                       a->beta, a->scale, a->shift, silu, (half_t*)y, ld_y, rows_per);
+    return check_launch("gn_apply_part");
   }
   if (!a->scale || !a->shift) return fail(SDK_EINVAL, "group_norm: scale/shift buffers needed");
   if (parts) {

@@ -199,7 +199,7 @@ class _Autotune:
     Enabled by ``enable()`` (UNetModel/AutoEncoderKL.prepare(autotune=True)); the
     first call of each distinct problem times every candidate (HIP events, 3 reps
     after a warm-up; SD_AMD_TUNE_REPS) and caches the fastest.  Never runs under graph capture."""
-    VARIANTS = (2, 5, 7, 6, 4, 3, 8, 9, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 31, 32, 33, 34)
+    VARIANTS = (2, 5, 7, 6, 4, 3, 8, 9, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 31, 32, 33, 34, 35)
     SPLITS = (0, 1, 2, 4, 8)
 
     def __init__(self):

@@ -561,3 +561,41 @@ def test_conv_direct_small_n(ops, B, H, W, Cin, Cout, k, pad, mode):
     with pytest.raises(RuntimeError):                      # does not fit: a 2-source concat
         ops.conv2d(pc, (x.to(DEV)[..., :Cin // 2].contiguous(), x.to(DEV)[..., Cin // 2:].contiguous()),
                    pad=pad, out_mode=om, variant=34)
+
+
+@pytest.mark.parametrize("M,K,N,silu,mode,res", [
+    (16, 320, 1280, False, "nhwc", False),     # time_embed[0] at the bench batch
+    (16, 1280, 1280, True, "nhwc", False),     # time_embed[2] (SiLU on the input)
+    (16, 1280, 20160, True, "rows", False),    # the 22 ResBlock emb projections, fp32 rows
+    (32, 1280, 2560, True, "rows", False),     # CFG-doubled batch
+    (7, 200, 72, False, "nhwc", True),         # ragged M / K / N, residual
+    (64, 96, 40, True, "rows", False),         # M = 64 (four row blocks)
+])
+def test_conv_skinny_rows(ops, M, K, N, silu, mode, res):
+    """Variant 35 (skinny GEMM for <= 64 rows: 16 columns per workgroup, K split over 4 waves,
+    v_mfma_f32_16x16x32_f16) vs fp32 torch; the planner picks it by itself at M <= 64."""
+    x = _rand(M, K, seed=M + K)
+    w = torch.randn(N, K) / math.sqrt(K)
+    b = torch.randn(N) * 0.1
+    pc = ops.PackedConv([(w, K)], b, device=DEV)
+    om = {"nhwc": ops.OUT_NHWC_F16, "rows": ops.OUT_ROWS_F32}[mode]
+    r = _rand(M, N, seed=3) if res else None
+    xd = x.to(DEV)
+    y = ops.linear(pc, xd, silu=silu, out_mode=om, residual=None if r is None else r.to(DEV))
+    x4 = xd.view(1, M, 1, K)
+    y35 = ops.conv2d(pc, x4, ksize=1, pad=0, silu=silu, out_mode=om, variant=35,
+                     residual=None if r is None else r.to(DEV).view(1, M, 1, N)).view(M, N)
+    assert torch.equal(y, y35), "the planner must pick the skinny variant for <= 64 rows"
+    xa = x.float()
+    if silu:
+        xa = F.silu(xa).half().float()
+    ref = xa @ w.half().float().t() + b
+    if r is not None:
+        ref = ref + r.float()
+    assert rel_l2(y.float().cpu(), ref) < 2e-3
+    if M > 8:   # the tiled kernels give the same numbers within fp32 summation order
+        yt = ops.conv2d(pc, x4, ksize=1, pad=0, silu=silu, out_mode=om, variant=0,
+                        residual=None if r is None else r.to(DEV).view(1, M, 1, N)).view(M, N)
+        assert rel_l2(y.float(), yt.float()) < 2e-3
+    with pytest.raises(RuntimeError):                      # does not fit: 65 rows
+        ops.conv2d(pc, _rand(1, 65, 1, K).to(DEV), ksize=1, pad=0, out_mode=om, variant=35)

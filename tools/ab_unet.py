@@ -22,7 +22,7 @@ def main():
     x = torch.randn(B, 4, 64, 64, generator=g).to(dev)
     ctx = torch.randn(B, 77, 768, generator=g).to(dev).half()
     t = torch.full((B,), 501, dtype=torch.long, device=dev)
-    tune = os.path.join(ROOT, "configs", "conv_tuning_mi355x.json")
+    tune = os.environ.get("TUNE", os.path.join(ROOT, "configs", "conv_tuning_mi355x.json"))
     if os.path.exists(tune):
         ops.AUTOTUNE.load(tune)
     arms = [dict(kv.split("=") for kv in a.split(",")) for a in sys.argv[1:]]
@@ -41,6 +41,8 @@ def main():
         with torch.cuda.graph(gr):
             y = unet(x, t, context=ctx)
         graphs.append((arm, gr, y))
+    if os.environ.get("SAVE_TUNE"):           # the next process of a cross-process A/B loads this table
+        ops.AUTOTUNE.save(os.environ["SAVE_TUNE"])
     res = {i: [] for i in range(len(graphs))}
     for rep in range(5):                      # interleaved: drift affects every arm alike
         for i, (arm, gr, _) in enumerate(graphs):
