@@ -1823,27 +1823,85 @@ int launch_ph(const Params& p, hipStream_t s) {
 }
 
 // Split-K reduction + epilogue: 8 columns per thread.
+// Slab sum of one (row, 8-column) octet: the slabs' 32-B pieces are loaded SK_U splits at a time
+// (independent loads in flight, instead of one dependent round trip per split) and added in split
+// order — a clamped slab past the end is loaded and selected away, never branched around (hipcc
+// would sink a conditional load under its branch and wait for each) — so the sum equals a plain loop's.
+constexpr int SK_U = 4;
+template <int NR>   // NR rows at once: their loads are in flight together
+__device__ __forceinline__ void slab_sum8(const Params& p, const int (&m)[NR], int n, float (&v)[NR][8]) {
+#pragma unroll
+  for (int q = 0; q < NR; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[q][j] = 0.f;
+  for (int s0 = 0; s0 < p.split; s0 += SK_U) {
+    f4 a[NR][SK_U], b[NR][SK_U];
+#pragma unroll
+    for (int u = 0; u < SK_U; ++u) {
+      const int su = min(s0 + u, p.split - 1);
+#pragma unroll
+      for (int q = 0; q < NR; ++q) {
+        const f4* src = reinterpret_cast<const f4*>(p.partial + ((size_t)su * p.M + m[q]) * p.Npad + n);
+        a[q][u] = src[0];
+        b[q][u] = src[1];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < SK_U; ++u) {
+      const bool in = s0 + u < p.split;
+#pragma unroll
+      for (int q = 0; q < NR; ++q)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[q][j] += in ? a[q][u][j] : 0.f;
+          v[q][4 + j] += in ? b[q][u][j] : 0.f;
+        }
+    }
+  }
+}
+
+// bias[n..n+7] + row_bias[b][n..n+7] as two vector loads each (scalar loads only for an unaligned
+// row_bias view), issued together instead of one dependent load per element
+__device__ __forceinline__ void epi_add8(const Params& p, int b, int n, float (&bi)[8], float (&rbv)[8]) {
+  f4 b0 = f4{}, b1 = f4{}, r0 = f4{}, r1 = f4{};
+  if (p.bias) {
+    const f4* q = reinterpret_cast<const f4*>(p.bias + n);
+    b0 = q[0];
+    b1 = q[1];
+  }
+  if (p.row_bias) {
+    const float* rb = p.row_bias + (size_t)b * p.rb_ld + n;
+    if (!((uintptr_t)rb & 15)) {
+      const f4* q = reinterpret_cast<const f4*>(rb);
+      r0 = q[0];
+      r1 = q[1];
+    } else {
+      r0 = f4{rb[0], rb[1], rb[2], rb[3]};
+      r1 = f4{rb[4], rb[5], rb[6], rb[7]};
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    bi[j] = b0[j];
+    bi[4 + j] = b1[j];
+    rbv[j] = r0[j];
+    rbv[4 + j] = r1[j];
+  }
+}
+
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(Params p) {
   const int groups = p.N / 8;
   const size_t total = (size_t)p.M * groups;
   for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
     const int m = (int)(e / groups), n = (int)(e - (size_t)m * groups) * 8;
-    float v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = 0.f;
-    for (int s = 0; s < p.split; ++s) {
-      const f4* src = reinterpret_cast<const f4*>(p.partial + ((size_t)s * p.M + m) * p.Npad + n);
-      f4 a = src[0], b = src[1];
-      v[0] += a[0]; v[1] += a[1]; v[2] += a[2]; v[3] += a[3];
-      v[4] += b[0]; v[5] += b[1]; v[6] += b[2]; v[7] += b[3];
-    }
+    float vv[1][8];
+    slab_sum8<1>(p, {m}, n, vv);
+    float (&v)[8] = vv[0];
     const int b = m / p.hw_out;
+    float bi[8], rbv[8];
+    epi_add8(p, b, n, bi, rbv);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if (p.bias) v[j] += p.bias[n + j];
-      if (p.row_bias) v[j] += p.row_bias[(size_t)b * p.rb_ld + n + j];
-      v[j] = act_fn(p.act, v[j]);
-    }
+    for (int j = 0; j < 8; ++j) v[j] = act_fn(p.act, (v[j] + bi[j]) + rbv[j]);
     if (p.out_mode == SDK_OUT_NHWC_F16) {
       h8 o;
 #pragma unroll
@@ -1881,31 +1939,32 @@ __global__ void __launch_bounds__(256) splitk_reduce_gn_kernel(Params p) {
   const int n = blockIdx.y * 64 + tc * 8;
   const bool colok = n < p.N;
   GnAcc ga;
-  for (int r = tr; r < R && colok; r += 32) {
-    const int m = b * p.hw_out + chunk * R + r;
-    float v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = 0.f;
-    for (int sp = 0; sp < p.split; ++sp) {
-      const f4* src = reinterpret_cast<const f4*>(p.partial + ((size_t)sp * p.M + m) * p.Npad + n);
-      const f4 a = src[0], c = src[1];
-      v[0] += a[0]; v[1] += a[1]; v[2] += a[2]; v[3] += a[3];
-      v[4] += c[0]; v[5] += c[1]; v[6] += c[2]; v[7] += c[3];
-    }
-    h8 o;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if (p.bias) v[j] += p.bias[n + j];
-      if (p.row_bias) v[j] += p.row_bias[(size_t)b * p.rb_ld + n + j];
-      o[j] = (half_t)act_fn(p.act, v[j]);
-    }
+  float bi[8], rbv[8];
+  if (colok) epi_add8(p, b, n, bi, rbv);   // the thread's columns and image are fixed
+  for (int r = tr; r < R && colok; r += 64) {   // rows r and r + 32 together
+    const bool two = r + 32 < R;
+    const int m0 = b * p.hw_out + chunk * R + r;
+    const int mm[2] = {m0, two ? m0 + 32 : m0};
+    h8 rr[2] = {h8{}, h8{}};
     if (p.res) {
-      const h8 rr = ldg16(p.res + (size_t)m * p.res_ld + n);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = (half_t)((float)o[j] + (float)rr[j]);
+      for (int q = 0; q < 2; ++q) rr[q] = ldg16(p.res + (size_t)mm[q] * p.res_ld + n);
     }
-    *reinterpret_cast<h8*>(reinterpret_cast<half_t*>(p.out) + (size_t)m * p.out_ld + n) = o;
-    gn_acc_add(ga, o, r == tr);
+    float v[2][8];
+    slab_sum8<2>(p, mm, n, v);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      if (q == 1 && !two) break;
+      h8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (half_t)act_fn(p.act, (v[q][j] + bi[j]) + rbv[j]);
+      if (p.res) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (half_t)((float)o[j] + (float)rr[q][j]);
+      }
+      *reinterpret_cast<h8*>(reinterpret_cast<half_t*>(p.out) + (size_t)mm[q] * p.out_ld + n) = o;
+      gn_acc_add(ga, o, r == tr && q == 0);
+    }
   }
   const int cnt = R > tr ? (R - tr + 31) / 32 : 0;
   if (cnt > 0 && colok) {
