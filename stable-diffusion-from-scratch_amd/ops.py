@@ -311,6 +311,51 @@ GN_ATTR = "_sd_gn_partial"
 EMIT_GN_STATS = True      # tests / A/B: False = every GroupNorm runs its own statistics pass
 
 
+# The LDS-DMA conv kernels address a source through a buffer resource (31-bit byte offsets); a source
+# of >= 2 GiB (the VAE decoder's 256-channel 512x512 maps at B=16: 2.15 GB) would push the plan onto
+# the register-staged kernel (~500 vs ~800 TFLOP/s).  Such convs run as batch chunks under the limit
+# (SD_AMD_CONV_CHUNK_LIMIT overrides it: A/B only).
+BUF_LIMIT = int(__import__("os").environ.get("SD_AMD_CONV_CHUNK_LIMIT", "2147483647"))
+
+
+def _src_bytes(x):
+    a, b = _as_pair(x)
+    B, H, W, _ = a.shape
+    ld = max(a.stride(2), b.stride(2) if b is not None else 0)
+    return B * H * W * ld * 2
+
+
+def _bslice(t, b0, b1):
+    if t is None:
+        return None
+    if isinstance(t, tuple):
+        return tuple(_bslice(u, b0, b1) for u in t)
+    return t[b0:b1]
+
+
+def _conv2d_batch_chunks(pc, x, seg2, gn, row_bias, residual, out, B, kw):
+    big = max(_src_bytes(x), _src_bytes(seg2[0]) if seg2 is not None else 0)
+    n = -(-big // BUF_LIMIT)
+    while big * 1.0 / n >= BUF_LIMIT or B % n:
+        n += 1
+        if n >= B:
+            n = B
+            break
+    cb = B // n
+    outs = []
+    for b0 in range(0, B, cb):
+        b1 = min(B, b0 + cb)
+        s2 = None if seg2 is None else (_bslice(seg2[0], b0, b1), _bslice(seg2[1], b0, b1), seg2[2])
+        rb = None if row_bias is None else (row_bias[0][b0:b1], row_bias[1])
+        outs.append(conv2d(pc, _bslice(x, b0, b1), seg2=s2, gn=_bslice(gn, b0, b1), row_bias=rb,
+                           residual=_bslice(residual, b0, b1), out=None if out is None else out[b0:b1], **kw))
+    full = out if out is not None else torch.cat(outs, 0)
+    parts = [getattr(o, GN_ATTR, None) for o in outs]
+    if all(pp is not None for pp in parts) and len({pp[1] for pp in parts}) == 1:
+        setattr(full, GN_ATTR, (torch.cat([pp[0] for pp in parts], 0), parts[0][1], full._version))
+    return full
+
+
 def conv2d(pc: PackedConv, x, *, ksize=None, stride=1, pad=None, pad_end=0, upsample=False, gn=None, silu=False,
            seg2=None, bias=True, row_bias=None, residual=None, out_mode=OUT_NHWC_F16, out=None,
            variant=None, split_k=None, act=ACT_NONE, gn_stats=False):
@@ -321,6 +366,22 @@ def conv2d(pc: PackedConv, x, *, ksize=None, stride=1, pad=None, pad_end=0, upsa
     or autotuner).  ``gn_stats``: the output feeds a GroupNorm — when the chosen plan can, the
     epilogue also emits its per-chunk channel statistics (attached to the returned tensor,
     consumed by ``group_norm``, which then skips its statistics pass)."""
+    B0 = _as_pair(x)[0].shape[0]
+    if B0 > 1 and (_src_bytes(x) >= BUF_LIMIT or (seg2 is not None and _src_bytes(seg2[0]) >= BUF_LIMIT)):
+        if out is None:
+            a0 = _as_pair(x)[0]
+            lh, lw = (2 * a0.shape[1], 2 * a0.shape[2]) if upsample else (a0.shape[1], a0.shape[2])
+            k_ = pc.seg_geom[0][0] if ksize is None else ksize
+            p_ = k_ // 2 if pad is None else pad
+            Ho = (lh + 2 * p_ + pad_end - k_) // stride + 1
+            Wo = (lw + 2 * p_ + pad_end - k_) // stride + 1
+            shape = {OUT_NHWC_F16: (B0, Ho, Wo, pc.N), OUT_GEGLU_F16: (B0, Ho, Wo, pc.N // 2),
+                     OUT_NCHW_F32: (B0, pc.N, Ho, Wo)}.get(out_mode, (B0, Ho, Wo, pc.N))
+            dt = torch.float16 if out_mode in (OUT_NHWC_F16, OUT_GEGLU_F16) else torch.float32
+            out = torch.empty(shape, dtype=dt, device=a0.device)
+        kw = dict(ksize=ksize, stride=stride, pad=pad, pad_end=pad_end, upsample=upsample, silu=silu, bias=bias,
+                  out_mode=out_mode, variant=variant, split_k=split_k, act=act, gn_stats=gn_stats)
+        return _conv2d_batch_chunks(pc, x, seg2, gn, row_bias, residual, out, B0, kw)
     a = ConvArgs()
     k0 = pc.seg_geom[0][0] if ksize is None else ksize
     if pad is None:

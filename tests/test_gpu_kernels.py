@@ -599,3 +599,36 @@ def test_conv_skinny_rows(ops, M, K, N, silu, mode, res):
         assert rel_l2(y.float(), yt.float()) < 2e-3
     with pytest.raises(RuntimeError):                      # does not fit: 65 rows
         ops.conv2d(pc, _rand(1, 65, 1, K).to(DEV), ksize=1, pad=0, out_mode=om, variant=35)
+
+
+def test_conv_batch_chunks_over_the_buffer_range(ops, monkeypatch):
+    """Sources of >= 2 GiB (the VAE decoder's 256-channel 512x512 maps at B=16) run as batch chunks
+    under the LDS-DMA kernels' 31-bit buffer range instead of falling back to the register-staged
+    kernel.  Forced here on a small problem by lowering ops.BUF_LIMIT: concat source + fused 1x1
+    segment + row bias + residual + GroupNorm statistics, vs the unchunked call."""
+    B, H, W = 4, 12, 12
+    g = torch.Generator(device="cpu").manual_seed(11)
+    xa, xb = _rand(B, H, W, 64, seed=1).to(DEV), _rand(B, H, W, 64, seed=2).to(DEV)
+    x2 = _rand(B, H, W, 64, seed=3).to(DEV)
+    w1 = torch.randn(192, 128, 3, 3, generator=g) / math.sqrt(128 * 9)
+    w2 = torch.randn(192, 64, 1, 1, generator=g) / 8.0
+    pc = ops.PackedConv([(w1, 128), (w2, 64)], torch.randn(192, generator=g), device=DEV)
+    emb = torch.randn(B, 200, generator=g).to(DEV)
+    res = _rand(B, H, W, 192, seed=4).to(DEV)
+    kw = dict(seg2=(x2, None, False), row_bias=(emb, 8), residual=res, gn_stats=True)
+    ref = ops.conv2d(pc, (xa, xb), **kw)
+    monkeypatch.setattr(ops, "BUF_LIMIT", B * H * W * 64 * 2 // 2 + 1)   # two chunks of 2 images
+    y = ops.conv2d(pc, (xa, xb), **kw)
+    assert y.shape == ref.shape
+    assert rel_l2(y, ref) < 1e-3
+    p_ref, p_y = getattr(ref, ops.GN_ATTR, None), getattr(y, ops.GN_ATTR, None)
+    assert (p_ref is None) == (p_y is None)
+    if p_y is not None:
+        assert p_y[0].shape == p_ref[0].shape and p_y[1] == p_ref[1]
+        assert torch.allclose(p_y[0][..., 0], p_ref[0][..., 0], rtol=1e-3, atol=1e-3)
+        gamma = torch.rand(192, generator=g).to(DEV) + 0.5
+        beta = torch.zeros(192).to(DEV)
+        assert rel_l2(ops.group_norm(y, gamma, beta, 1e-6, 32), ops.group_norm(ref, gamma, beta, 1e-6, 32)) < 2e-3
+    yn = ops.conv2d(pc, (xa, xb), seg2=(x2, None, False), out_mode=ops.OUT_NCHW_F32)
+    monkeypatch.setattr(ops, "BUF_LIMIT", 2147483647)
+    assert rel_l2(yn, ops.conv2d(pc, (xa, xb), seg2=(x2, None, False), out_mode=ops.OUT_NCHW_F32)) < 1e-3
