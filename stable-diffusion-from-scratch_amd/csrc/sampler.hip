@@ -369,6 +369,22 @@ extern "C" const char* sdk_kernel_name(int32_t variant) {
     case 7: return "conv_glds_kernel<Cfg<128,320,4,2>>";
     case 8: return "conv_ph_kernel<256x256,ring8>";
     case 9: return "conv_ph_kernel<256x256,ring10>";
+    case 16: return "conv_glds_kernel<Cfg<128,128,2,2,4>>";
+    case 17: return "conv_glds_kernel<Cfg<256,128,4,2,3>>";
+    case 18: return "conv_glds_kernel<Cfg<128,128,2,2,3>>";
+    case 19: return "conv_glds_kernel<Cfg<128,256,2,4,3>>";
+    case 20: return "conv_ph_kernel<256x256,ring8,m16>";
+    case 21: return "conv_ph_kernel<256x256,ring10,m16>";
+    case 22: return "conv_glds_kernel<Cfg<256,320,8,2,2,m16>>";
+    case 23: return "conv_glds_kernel<Cfg<128,320,4,2,2,m16>>";
+    case 24: return "conv_glds_kernel<Cfg<256,160,8,1,2,m16>>";
+    case 25: return "conv_glds_kernel<Cfg<128,256,2,4,3,m16>>";
+    case 26: return "conv_glds_kernel<Cfg<128,128,2,2,3,m16>>";
+    case 31: return "conv_glds_kernel<Cfg<128,160,4,1,2,m16,occ2>>";
+    case 32: return "conv_glds_kernel<Cfg<128,128,2,2,2,m16,occ2>>";
+    case 33: return "conv_glds_kernel<Cfg<128,160,4,1,4,m16>>";
+    case 34: return "conv_direct_kernel";
+    case 35: return "conv_skinny_kernel";
     default: return "unknown";
   }
 }

@@ -54,6 +54,33 @@ def test_conv_plan_validates_on_host(sdk):
     assert L.sdk_conv2d_plan(C.byref(a), C.byref(info)) != 0       # geometry mismatch
 
 
+def test_conv_plan_picks_skinny_and_names_every_variant(sdk):
+    """The host planner routes <= 64-row 1x1 GEMMs (the time-embedding MLP at M = batch) to the skinny
+    kernel (variant 35) and larger ones to the tiled kernels; sdk_kernel_name knows every variant id
+    the autotuner may choose."""
+    from sd_amd import _lib, ops
+    L = sdk.library()
+    L.sdk_kernel_name.restype = C.c_char_p
+    for v in ops.AUTOTUNE.VARIANTS + (0,):
+        assert L.sdk_kernel_name(v) != b"unknown", v
+    a = _lib.ConvArgs()
+    info = _lib.ConvPlanInfo()
+    a.batch, a.ho, a.wo, a.cout, a.nseg = 1, 16, 1, 1280, 1
+    s = a.seg[0]
+    s.src0 = 0x1000; s.c_split = 320; s.cin = 320; s.ld0 = 320; s.h = 16; s.w = 1
+    s.ksize = 1; s.stride = 1; s.pad = 0
+    a.weight = 0x2000; a.out = 0x3000; a.out_ld = 1280; a.k_total = 320
+    assert L.sdk_conv2d_plan(C.byref(a), C.byref(info)) == 0, L.sdk_last_error()
+    assert info.variant == 35 and info.split_k == 1 and info.workspace_bytes == 0
+    a.ho = s.h = 65                                    # 65 rows: a tiled plan
+    assert L.sdk_conv2d_plan(C.byref(a), C.byref(info)) == 0, L.sdk_last_error()
+    assert info.variant != 35
+    a.variant_hint = 36
+    assert L.sdk_conv2d_plan(C.byref(a), C.byref(info)) != 0         # forced 35 on 65 rows
+    a.variant_hint = 37
+    assert L.sdk_conv2d_plan(C.byref(a), C.byref(info)) != 0         # unknown id
+
+
 def test_group_norm_workspace(sdk):
     L = sdk.library()
     assert L.sdk_group_norm_workspace(2, 4096, 320) > 0
