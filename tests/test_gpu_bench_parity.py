@@ -126,6 +126,21 @@ def test_bench_config_short_sample_and_decode_deterministic(bench_c3):
     assert torch.equal(a, b)
 
 
+def test_bench_config_decode_b16_batch_chunks_vs_single_images(bench_c3):
+    """The bench's B=16 decode runs the 256-channel 512x512 convs as batch chunks (their sources pass
+    the 2 GiB buffer range: ops.BUF_LIMIT); images 0 and 15 of it vs the same latents decoded alone
+    (B=1, no chunking) with the same tuning table."""
+    ld = bench_c3["ld"]
+    from sd_amd import ops
+    z = torch.randn(16, 4, 64, 64, generator=torch.Generator().manual_seed(77)).to(DEV)
+    assert 16 * 512 * 512 * 256 * 2 >= ops.BUF_LIMIT
+    full = ld.decode_first_stage(z)
+    assert full.shape == (16, 3, 512, 512) and torch.isfinite(full).all()
+    for i in (0, 15):
+        one = ld.decode_first_stage(z[i:i + 1].contiguous())
+        assert rel_l2(full[i:i + 1], one) < 2e-3, i
+
+
 # ------------------------------------------------------------------ cache soundness
 def _tiny_ld(graphs):
     import yaml
