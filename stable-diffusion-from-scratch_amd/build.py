@@ -31,7 +31,7 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False) -> str
     bdir = BUILD + ("_diag" if diag else "")
     lib = LIB.replace(".so", "_diag.so") if diag else LIB
     os.makedirs(bdir, exist_ok=True)
-    headers = [os.path.join(CSRC, "common.h"), os.path.join(HERE, "..", "include", "sdk_amd.h")]
+    headers = [os.path.join(CSRC, "common.h"), os.path.join(CSRC, "halo_sched.h"), os.path.join(HERE, "..", "include", "sdk_amd.h")]
     jobs = []
     for src in SOURCES:
         s = os.path.join(CSRC, src)

@@ -23,6 +23,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "halo_sched.h"
 
 namespace sdk {
 namespace {
@@ -67,6 +68,10 @@ struct Params {
                         // the LDS-DMA A gather is a lane base + a scalar tap offset, no masks
   float2* gnp;          // GroupNorm statistics of the fp16 output: [batch][gn_nch][N] (mean, M2) over
   int gn_nch;           // hw_out / gn_nch rows each (one chunk = one M-tile, or 64 rows of the split-K reduce)
+  // halo-tile 3x3 kernel (variants 36, 37; halo_sched.h): halo row stride (px), pieces per channel
+  // block, ring slots, issue schedule
+  int h_hs, h_np, h_rp;
+  int h_phi[10];
 };
 
 // epilogue activation (CLIP's quick_gelu x*sigmoid(1.702x), transformers activations.py QuickGELUActivation)
@@ -1399,6 +1404,203 @@ using Cfg128x160o2m = Cfg<128, 160, 4, 1, 2, true, 2>;
 using Cfg128x128o2m = Cfg<128, 128, 2, 2, 2, true, 2>;
 using Cfg128x160r4m = Cfg<128, 160, 4, 1, 4, true>;      // one workgroup, 3 K-steps of DMA in flight
 
+// ---------------------------------------------------------------------- halo-tile 3x3 kernel
+// Variants 36 (256x320 tile, 16 waves 8x2) and 37 (128x320, 8 waves 4x2), v_mfma_f32_16x16x32_f16.
+// For a 3x3 pad-0 conv over a zero-bordered image (the GN+SiLU output of gn_apply_pad_kernel) the A
+// operand of all nine taps of a 64-channel block comes from ONE staged span of padded input rows
+// (halo_sched.h): ~np 1-KiB DMA pieces per block instead of 9 * TBM / 8, and the activation leaves
+// L2 once per block instead of nine times (SD 64x64 level, 256-pixel tile: 50 pieces vs 288).
+// W tiles stream per K-step through a 2-stage ring as in conv_glds_kernel; halo pieces stream
+// through a ring of rp slots on the host-planned schedule (the pieces of block cb+1 land while
+// block cb computes, each in the slot of a piece that is already dead).  A wave's DMA count per
+// K-step varies (its W pieces + that K-step's halo pieces), so the counted vmcnt wait is picked at
+// run time from a wave-uniform count.  Fragment reads: halo pixel h of the block sits in slot
+// (cb * np + h / 8) % rp, row h % 8, 16-B chunks XOR-swizzled with (h >> 1) & 7 (the DMA source
+// carries the same permutation) — 16 consecutive pixels hit 16 distinct bank groups.
+template <int TBM_, int TBN_, int WM_, int WN_>
+struct HCfg {
+  static constexpr int TBM = TBM_, TBN = TBN_, WM = WM_, WN = WN_;
+  static constexpr int NW = WM * WN, NT = NW * 64;
+  static constexpr int TM = TBM / WM, TN = TBN / WN;
+  static constexpr int FM16 = TM / 16, FN16 = TN / 16;
+  static constexpr int WPIECES = TBN / 8;                 // 1-KiB W pieces per K-step
+  static constexpr int WPW = (WPIECES + NW - 1) / NW;     // per wave (the last waves may issue one fewer)
+  static constexpr int WSTAGE_H = TBN * BK;               // halfs per W stage
+  static constexpr int WRING_BYTES = 2 * WSTAGE_H * 2;
+  static constexpr int VEC_BYTES = 2 * TBN * 4;           // staged bias / embedding row
+  static constexpr int MAX_RP = (160 * 1024 - WRING_BYTES - VEC_BYTES) / 1024;
+  static_assert(WRING_BYTES / NW >= EPG_BYTES + TM / 16 * TN * 8, "per-wave epilogue scratch in the W ring");
+  static_assert(TBN <= NT && TBN % 8 == 0 && TM % 16 == 0 && TN % 16 == 0, "tile shape");
+};
+using HCfg256x320 = HCfg<256, 320, 8, 2>;
+using HCfg128x320 = HCfg<128, 320, 4, 2>;
+
+// s_waitcnt vmcnt(n) for a wave-uniform run-time n (waiting for fewer outstanding DMAs than needed
+// is only slower, so counts past the table wait for 12)
+__device__ __forceinline__ void vmcnt_wait_dyn(int n) {
+  switch (n) {
+#define SDK_VW(N) \
+  case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+    SDK_VW(0) SDK_VW(1) SDK_VW(2) SDK_VW(3) SDK_VW(4) SDK_VW(5) SDK_VW(6) SDK_VW(7) SDK_VW(8) SDK_VW(9)
+    SDK_VW(10) SDK_VW(11)
+#undef SDK_VW
+    default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  }
+}
+
+template <class CF>
+__global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_halo_kernel(Params p) {
+  extern __shared__ __attribute__((aligned(16))) half_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / CF::WN, wn = wave % CF::WN;
+  const int nitems = p.tiles_m * p.tiles_n * p.split;
+  const int it = xcd_remap((int)blockIdx.x + (int)blockIdx.y * (int)gridDim.x, nitems);
+  int tm, tn, sidx;
+  item_coords(p, it, tm, tn, sidx);
+  const int m0 = tm * CF::TBM, n0 = tn * CF::TBN;
+  const int kt0 = sidx * p.kt_per_split, kt1 = min(p.kt_total, kt0 + p.kt_per_split);   // multiples of 9
+  const int lrow = lane >> 3;
+  const Seg& g0 = p.seg[0];
+  const DmaSrc d = make_dma_src(p);
+  const int NP = p.h_np, RP = p.h_rp, HS = p.h_hs;
+  half_t* const halo = lds + 2 * CF::WSTAGE_H;
+  // the tile's halo: whole padded rows from the first output row it touches (whole images when a
+  // tile holds several)
+  const int b0 = m0 / p.hw_out;
+  const int oy0 = (m0 - b0 * p.hw_out) / p.wo;
+  const int hstart = (b0 * g0.h + oy0) * g0.w;
+  const int r16 = lane & 15, c16 = lane >> 4;
+  // halo pixel of each A fragment row (tap (0, 0)); rows past M read a valid pixel, never stored
+  int hb[CF::FM16];
+#pragma unroll
+  for (int i = 0; i < CF::FM16; ++i) {
+    const int m = min(m0 + wm * CF::TM + i * 16 + r16, p.M - 1);
+    const int b = m / p.hw_out, rem = m - b * p.hw_out;
+    const int oy = rem / p.wo, ox = rem - oy * p.wo;
+    hb[i] = ((b - b0) * g0.h + oy - oy0) * HS + ox;
+  }
+  // W pieces of this wave: tile rows 8 * (wave + NW * i) + lrow
+  unsigned wv[CF::WPW];
+#pragma unroll
+  for (int i = 0; i < CF::WPW; ++i) {
+    const int piece = wave + CF::NW * i;
+    const int rch = (lane & 7) ^ ((4 * piece + (lrow >> 1)) & 7);
+    wv[i] = piece < CF::WPIECES ? w_row_ctx(p, n0 + piece * 8 + lrow, rch) : PH_OOB;
+  }
+  const int wcnt = wave < CF::WPIECES ? (CF::WPIECES - wave + CF::NW - 1) / CF::NW : 0;
+  auto issue_w = [&](int kt, int stage) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < CF::WPW; ++i)
+      if (i < wcnt) ph_dma(d.w, lds + stage * CF::WSTAGE_H + (wave + CF::NW * i) * 8 * BK, wv[i], kt * BK * 2);
+  };
+  // halo stream: global piece g = cb * NP + q, issued by wave (g - cb0 * NP) % NW into slot g % RP
+  const int cb0 = kt0 / 9;
+  const int gend = ((kt1 + 8) / 9) * NP;
+  int gw = cb0 * NP + wave, cbw = cb0, qw = wave, sw = gw % RP;   // this wave's next piece (NW <= NP)
+  auto issue_halo = [&](int hi) __attribute__((always_inline)) {
+    int n = 0;
+    while (gw < hi) {
+      const int c = cbw * BK;
+      const bool second = c >= g0.c_split;
+      const unsigned ld2 = (unsigned)(second ? g0.ld1 : g0.ld0) * 2u;
+      const int cc = c - (second ? g0.c_split : 0);
+      const int rchh = (lane & 7) ^ ((4 * qw + (lrow >> 1)) & 7);
+      const unsigned voff = (unsigned)(hstart + 8 * qw + lrow) * ld2 + (unsigned)(cc + rchh * 8) * 2u;
+      ph_dma(second ? d.a1 : d.a0, halo + sw * 512, voff, 0);
+      ++n;
+      gw += CF::NW;
+      qw += CF::NW;
+      if (qw >= NP) { qw -= NP; ++cbw; }
+      sw += CF::NW;
+      if (sw >= RP) sw -= RP;
+    }
+    return n;
+  };
+  const EpiVec ev = epi_vec_load(p, m0, n0, CF::TBM, CF::TBN);
+
+  f4 acc16[CF::FM16][CF::FN16];
+#pragma unroll
+  for (int i = 0; i < CF::FM16; ++i)
+#pragma unroll
+    for (int j = 0; j < CF::FN16; ++j) acc16[i][j] = f4{};
+  const int brow16 = wn * CF::TN + r16;
+
+  // prologue: W of the first K-step, the first block's early halo pieces
+  issue_w(kt0, 0);
+  issue_halo(min(gend, cb0 * NP + p.h_phi[0]));
+  int cb = cb0, j = 0;
+  int cbslot = (cb0 * NP) % RP;   // slot of the current block's piece 0
+#if !defined(SDK_NO_PRIO)
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= CF::NT / 2) __builtin_amdgcn_s_setprio(1);
+#endif
+  for (int kt = kt0; kt < kt1; ++kt) {
+    int n = 0;
+    if (kt + 1 < kt1) {
+      issue_w(kt + 1, (kt + 1 - kt0) & 1);
+      n = wcnt;
+    }
+    n += issue_halo(min(gend, cb * NP + p.h_phi[j + 1]));
+    vmcnt_wait_dyn(__builtin_amdgcn_readfirstlane(n));
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    const half_t* st = lds + ((kt - kt0) & 1) * CF::WSTAGE_H;
+    const int ky = j / 3, toff = ky * HS + (j - 3 * ky);
+    const half_t* ab[CF::FM16];
+    int sx[CF::FM16];
+#pragma unroll
+    for (int i = 0; i < CF::FM16; ++i) {
+      const int h = hb[i] + toff;
+      int slot = cbslot + (h >> 3);
+      slot -= slot >= RP ? RP : 0;
+      ab[i] = halo + slot * 512 + (h & 7) * 64;
+      sx[i] = (h >> 1) & 7;
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      h8 fa[CF::FM16];
+#pragma unroll
+      for (int i = 0; i < CF::FM16; ++i) fa[i] = *reinterpret_cast<const h8*>(ab[i] + (((kk * 4 + c16) ^ sx[i]) << 3));
+#pragma unroll
+      for (int jj = 0; jj < CF::FN16; ++jj) {
+        const h8 fb = *reinterpret_cast<const h8*>(st + swz(brow16 + jj * 16, kk * 4 + c16));
+#pragma unroll
+        for (int i = 0; i < CF::FM16; ++i)
+          acc16[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb, fa[i], acc16[i][jj], 0, 0, 0);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();      // everyone done reading this K-step's W stage and halo slots
+    __builtin_amdgcn_sched_barrier(0);
+    if (++j == 9) {
+      j = 0;
+      ++cb;
+      cbslot += NP;
+      cbslot -= cbslot >= RP ? RP : 0;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float* vec_s = reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + CF::WRING_BYTES + RP * 1024);
+  epi_vec_store(ev, vec_s, CF::TBN);
+  __builtin_amdgcn_s_barrier();
+  const float* bias_s = p.bias ? vec_s : nullptr;
+  const float* rb_s = ev.one_img ? vec_s + CF::TBN : nullptr;
+  constexpr int WSCR = CF::WRING_BYTES / CF::NW / 16 * 8;   // per-wave epilogue scratch (halfs) in the W ring
+  half_t* wscr = lds + wave * WSCR;
+  const bool lds_epi = p.split == 1 && p.out_mode == SDK_OUT_NHWC_F16;
+  if (lds_epi && p.gnp) {
+    epilogue16_tile<CF::FM16, CF::FN16, true>(p, acc16, m0, n0, wm * CF::TM, wn * CF::TN, wscr, bias_s, rb_s);
+    __syncthreads();
+    gn_tile_store<CF::WM, CF::WN, CF::TN, CF::TM / 16, 16, CF::TBM, CF::TBN>(
+        p, m0, n0, [&](int w) { return reinterpret_cast<const float2*>(lds + w * WSCR + EPG_BYTES / 2); });
+  } else if (lds_epi) {
+    epilogue16_tile<CF::FM16, CF::FN16>(p, acc16, m0, n0, wm * CF::TM, wn * CF::TN, wscr, bias_s, rb_s);
+  } else {
+    epilogue16_tile_direct<CF::FM16, CF::FN16>(p, acc16, m0, n0, wm * CF::TM, wn * CF::TN, sidx);
+  }
+}
+
 
 // ---------------------------------------------------------------------- 16x16x32 epilogues
 // Transposed 16x16 accumulator (D^T = W A^T, v_mfma_f32_16x16x32_f16): lane l holds pixel
@@ -2199,6 +2401,17 @@ int launch_glds(const Params& p, hipStream_t s) {
   return check_launch("conv_glds");
 }
 
+template <class CF>
+int launch_halo(const Params& p, hipStream_t s) {
+  static std::atomic<unsigned long long> attr_set{0};
+  if (p.h_rp <= 0 || p.h_rp > CF::MAX_RP || p.h_np > p.h_rp || p.kt_per_split % 9 || p.kt_total % 9)
+    return fail(SDK_EINVAL, "conv2d: halo plan out of range");
+  const int lds_bytes = CF::WRING_BYTES + p.h_rp * 1024 + CF::VEC_BYTES;
+  if (int e = ensure_dyn_lds((const void*)conv_halo_kernel<CF>, 160 * 1024, attr_set, "conv2d")) return e;
+  hipLaunchKernelGGL((conv_halo_kernel<CF>), dim3(p.tiles_m * p.tiles_n, p.split), dim3(CF::NT), lds_bytes, s, p);
+  return check_launch("conv_halo");
+}
+
 #ifdef SDK_CONV_DIAGNOSTICS
 constexpr bool kDiagnostics = true;
 #else
@@ -2380,6 +2593,62 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
       return SDK_OK;
     }
   }
+  // variants 36 / 37: halo-tile 3x3 (256x320 / 128x320 tiles) for a pad-0 3x3 conv over a zero-bordered
+  // image (nomask, one segment); a plan exists when the tile's padded rows fit the LDS ring on time
+  // (halo_sched.h).  Forced but not applicable: the planner's choice, as for the other variants.
+  if (forced == 36 || forced == 37) {
+    const sdk_conv_src& g = a->seg[0];
+    const bool shape_ok = !transform && a->nseg == 1 && g.ksize == 3 && g.stride == 1 && g.pad == 0 &&
+                          g.pad_end == 0 && !g.upsample && p.nomask && a->out_mode != SDK_OUT_GEGLU_F16;
+    const int tbm = forced == 36 ? HCfg256x320::TBM : HCfg128x320::TBM;
+    const int tbn = HCfg256x320::TBN;
+    const int nw = forced == 36 ? HCfg256x320::NW : HCfg128x320::NW;
+    const int max_rp = forced == 36 ? HCfg256x320::MAX_RP : HCfg128x320::MAX_RP;
+    HaloPlan hp;
+    if (shape_ok && halo_plan(p.hw_out, p.ho, p.wo, g.h, g.w, tbm, max_rp, nw, &hp) == 0) {
+      p.variant = forced;
+      p.tiles_m = (p.M + tbm - 1) / tbm;
+      p.tiles_n = (p.N + tbn - 1) / tbn;
+      p.Npad = p.tiles_n * tbn;
+      p.h_hs = hp.hs;
+      p.h_np = hp.np;
+      p.h_rp = hp.rp;
+      for (int j = 0; j < 10; ++j) p.h_phi[j] = hp.phi[j];
+      const int ncb = kt / 9, tiles = p.tiles_m * p.tiles_n;
+      int split = a->split_k;
+      if (split <= 0) {
+        split = 1;
+        while (tiles * split < 256 && ncb / (split * 2) >= 2 && split < 16) split *= 2;
+      }
+      if (a->cout % 8) split = 1;
+      split = std::max(1, std::min(split, ncb));
+      p.kt_per_split = 9 * ((ncb + split - 1) / split);   // splits on channel-block boundaries
+      split = (kt + p.kt_per_split - 1) / p.kt_per_split;
+      p.split = split;
+      const int64_t ws = split > 1 ? (int64_t)split * p.M * p.Npad * 4 : 0;
+      int gn_nch = 0;
+      if (a->out_mode == SDK_OUT_NHWC_F16) {
+        if (split > 1) gn_nch = p.hw_out % 64 == 0 ? p.hw_out / 64 : 1;
+        else if (p.hw_out % tbm == 0) gn_nch = p.hw_out / tbm;
+      }
+      if (info) {
+        info->split_k = split;
+        info->grid_tiles = tiles;
+        info->workspace_bytes = ws;
+        info->variant = forced;
+        info->flops = 2.0 * p.M * (double)p.N * kreal;
+        info->gn_chunks = gn_nch;
+      }
+      if (split > 1) p.partial = a->workspace;
+      if (a->gn_partial) {
+        if (gn_nch == 0)
+          return fail(SDK_EINVAL, "conv2d: this plan emits no GroupNorm statistics (sdk_conv_plan_info.gn_chunks == 0)");
+        p.gnp = reinterpret_cast<float2*>(a->gn_partial);
+        p.gn_nch = gn_nch;
+      }
+      return SDK_OK;
+    }
+  }
   // ids: 0 register-staged; 2..7 LDS-DMA configs; 8, 9 phased 256x256; 10..15 diagnostics;
   // 16..19 deep-ring LDS-DMA configs; 20, 21 phased 256x256 on v_mfma_f32_16x16x32_f16;
   // 22..26 LDS-DMA configs 5, 7, 6, 19, 18 on v_mfma_f32_16x16x32_f16; 27..30 diagnostics;
@@ -2389,7 +2658,7 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   if (is_diagnostic_variant(forced) && !kDiagnostics)
     return fail(SDK_EINVAL, "conv2d: variant " + std::to_string(forced) +
                                 " is a diagnostic ablation (only in libsdk_amd_diag.so)");
-  if (forced > 35 || forced == 1) return fail(SDK_EINVAL, "conv2d: unknown variant " + std::to_string(forced));
+  if (forced > 37 || forced == 1) return fail(SDK_EINVAL, "conv2d: unknown variant " + std::to_string(forced));
   const int fbase = forced;
   const bool fvalid = forced >= 0 && forced != 1 && forced <= 33;
   const bool fgeglu = (fbase <= 4 || fbase >= 8) && fbase != 22 && fbase != 23 && fbase != 24 && fbase != 31 &&
@@ -2508,6 +2777,8 @@ extern "C" int sdk_conv2d(const sdk_conv_args* a, sdk_stream_t stream) {
     case 33: rc = launch_glds<Cfg128x160r4m>(p, s); break;
     case 34: rc = launch_direct(p, s); break;
     case 35: rc = launch_skinny(p, s); break;
+    case 36: rc = launch_halo<HCfg256x320>(p, s); break;
+    case 37: rc = launch_halo<HCfg128x320>(p, s); break;
 #ifdef SDK_CONV_DIAGNOSTICS
     case 27: rc = launch_ph<PhCfg8, 128>(p, s); break;   // diagnostics: no W DMA issued
     case 28: rc = launch_ph<PhCfg8, 256>(p, s); break;   // diagnostics: no A DMA issued

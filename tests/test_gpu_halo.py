@@ -1,0 +1,110 @@
+"""Halo-tile 3x3 conv (conv.hip conv_halo_kernel, variants 36 / 37) on the MI355X (run with -m gpu).
+
+The halo kernel stages the padded input rows of a tile once per 64-channel block and forms the nine
+taps from LDS; its K order, wave tiling and MFMA shape equal the LDS-DMA configs 22 (256x320) and
+23 (128x320), so its outputs must be BITWISE equal to theirs, and within the fp16 tolerance of an
+fp32 conv of the same fp16 inputs (rel-L2 <= 2e-3).  Shapes cover the SD levels (64x64, 32x32,
+16x16 single-image tiles; 8x8 multi-image tiles), split-K on channel-block boundaries, a ragged last
+tile (batch not a multiple of the images per tile), a 2-source concat, the embedding row, the
+residual and the GroupNorm statistics emitted by the epilogue."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from gpu_util import rel_l2
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+TWIN = {36: 22, 37: 23}
+
+
+@pytest.fixture(scope="module")
+def ops(sdk):
+    from sd_amd import ops as o
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    return o
+
+
+def _rand(*shape, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(*shape, generator=g).half()
+
+
+def _ran(ops, fn):
+    """(result, variant the plan ran) of one conv call."""
+    ops.PROFILER.start()
+    try:
+        y = fn()
+    finally:
+        ops.PROFILER.stop()
+    return y, ops.PROFILER.records[-1][1]
+
+
+def _padded(x):
+    return F.pad(x.float().permute(0, 3, 1, 2), (1, 1, 1, 1)).permute(0, 2, 3, 1).half().contiguous()
+
+
+@pytest.mark.parametrize("variant", [36, 37])
+@pytest.mark.parametrize("B,H,W,Ci,Co,split", [
+    (2, 64, 64, 320, 320, 1),       # SD 64x64 level
+    (2, 32, 32, 640, 640, 1),       # 32x32
+    (2, 16, 16, 1280, 1280, 4),     # 16x16, split-K over channel blocks
+    (3, 8, 8, 128, 320, 1),         # multi-image tiles, ragged last tile
+    (1, 16, 16, 128, 320, 2),       # one channel block per split
+    (2, 48, 48, 192, 320, 1),       # C5-shaped level (tiles not row-aligned)
+])
+def test_halo_conv_matches_twin_and_fp32(ops, variant, B, H, W, Ci, Co, split):
+    x = _rand(B, H, W, Ci, seed=H + Ci)
+    w = torch.randn(Co, Ci, 3, 3, generator=torch.Generator().manual_seed(Co)) / math.sqrt(Ci * 9)
+    b = torch.randn(Co, generator=torch.Generator().manual_seed(Co + 1)) * 0.1
+    pc = ops.PackedConv([(w, Ci)], b, device=DEV)
+    xp = _padded(x).to(DEV)
+    y, ran = _ran(ops, lambda: ops.conv2d(pc, xp, pad=0, variant=variant, split_k=split))
+    if ran != variant:
+        assert (variant, H) == (36, 8), "the halo plan should exist for this shape"
+        pytest.skip("4 images per 256-pixel tile overflow the ring: the planner runs")
+    yt = ops.conv2d(pc, xp, pad=0, variant=TWIN[variant], split_k=split)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.half().float(), b, padding=1).permute(0, 2, 3, 1)
+    assert y.shape == ref.shape
+    assert rel_l2(y, ref) < 2e-3
+    assert torch.equal(y, yt), f"variant {variant} differs from its LDS-DMA twin {TWIN[variant]}"
+
+
+@pytest.mark.parametrize("variant", [36, 37])
+def test_halo_plan_is_taken(ops, variant):
+    """The plan really runs the halo kernel (not a fallback) on an applicable shape, and falls back
+    to the planner on one it cannot take (a masked pad-1 conv)."""
+    x = _rand(2, 16, 16, 64, seed=5)
+    w = torch.randn(320, 64, 3, 3) / 24
+    pc = ops.PackedConv([(w, 64)], None, device=DEV)
+    _, r0 = _ran(ops, lambda: ops.conv2d(pc, _padded(x).to(DEV), pad=0, variant=variant))
+    _, r1 = _ran(ops, lambda: ops.conv2d(pc, x.to(DEV), pad=1, variant=variant))
+    assert r0 == variant and r1 != variant
+
+
+@pytest.mark.parametrize("variant", [36, 37])
+def test_halo_concat_rowbias_residual_gn_stats(ops, variant):
+    """Two-source concat input (c_split a multiple of 64), the per-image embedding row, the residual
+    add and the emitted GroupNorm statistics — the ResBlock conv's full epilogue."""
+    B, H, W, C1, C2, Co = 2, 32, 32, 128, 192, 320
+    a, c = _rand(B, H, W, C1, seed=7), _rand(B, H, W, C2, seed=8)
+    ap, cp = _padded(a).to(DEV), _padded(c).to(DEV)
+    g = torch.Generator().manual_seed(11)
+    w = torch.randn(Co, C1 + C2, 3, 3, generator=g) / math.sqrt((C1 + C2) * 9)
+    b = torch.randn(Co, generator=g) * 2 + 3
+    emb = torch.randn(B, Co + 8, generator=g)
+    res = _rand(B, H, W, Co, seed=9)
+    pc = ops.PackedConv([(w, C1 + C2)], b, device=DEV)
+    kw = dict(pad=0, row_bias=(emb.to(DEV), 8), residual=res.to(DEV), gn_stats=True, split_k=1)
+    y, ran = _ran(ops, lambda: ops.conv2d(pc, (ap, cp), variant=variant, **kw))
+    assert ran == variant
+    yt = ops.conv2d(pc, (ap, cp), variant=TWIN[variant], **kw)
+    xcat = torch.cat([a, c], -1).float().permute(0, 3, 1, 2)
+    ref = F.conv2d(xcat, w.half().float(), b, padding=1).permute(0, 2, 3, 1) + emb[:, None, None, 8:] + res.float()
+    assert rel_l2(y, ref) < 3e-3
+    assert torch.equal(y, yt)
+    pp, nch, _ = getattr(y, ops.GN_ATTR)
+    pt, ncht, _ = getattr(yt, ops.GN_ATTR)
+    assert nch == ncht and torch.equal(pp, pt)

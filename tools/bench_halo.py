@@ -1,0 +1,67 @@
+"""Halo-tile 3x3 conv (variants 36 / 37) vs the LDS-DMA configs on the SD UNet 3x3 shapes at B=16
+(zero-bordered input, pad 0 — the GN+SiLU output the ResBlock convs read).  Device time per launch
+from a HIP graph of back-to-back launches (host marshalling excluded), median of 7, random data.
+usage: python tools/bench_halo.py [variants] [splits]"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from tools.sweep_shape import graph_us  # noqa: E402
+
+SHAPES = [  # B, H, W, Cin, Cout (3x3, stride 1)
+    (16, 64, 64, 320, 320),
+    (16, 64, 64, 640, 320),
+    (16, 64, 64, 960, 320),
+    (16, 32, 32, 320, 640),
+    (16, 32, 32, 640, 640),
+    (16, 32, 32, 1280, 640),
+    (16, 32, 32, 1920, 640),
+    (16, 16, 16, 640, 1280),
+    (16, 16, 16, 1280, 1280),
+    (16, 16, 16, 2560, 1280),
+    (8, 96, 96, 320, 320),
+    (8, 48, 48, 640, 640),
+]
+
+
+def main():
+    import sd_amd_loader
+    sd_amd_loader.load()
+    from sd_amd import ops
+    variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "22,23,5,8,20,36,37").split(",")]
+    splits = [int(v) for v in (sys.argv[2] if len(sys.argv) > 2 else "1,2,4,8").split(",")]
+    for B, H, W, Ci, Co in SHAPES:
+        torch.manual_seed(0)
+        xp = torch.randn(B, H + 2, W + 2, Ci, device="cuda").half()
+        w = torch.randn(Co, Ci, 3, 3, device="cuda") / (Ci * 9) ** 0.5
+        pc = ops.PackedConv([(w, Ci)], torch.zeros(Co, device="cuda"), device="cuda")
+        flop = 2.0 * B * H * W * Co * Ci * 9
+        res = []
+        for var in variants:
+            for sp in splits:
+                f = lambda: ops.conv2d(pc, xp, pad=0, variant=var, split_k=sp)   # noqa: E731
+                try:
+                    ops.PROFILER.start()
+                    f()
+                    ops.PROFILER.stop()
+                    info = ops.PROFILER.records[-1][5]
+                    if ops.PROFILER.records[-1][1] != var or (info and info[4] != sp):
+                        continue                  # the forced plan does not apply: the planner ran
+                    us = graph_us(f)
+                except RuntimeError:
+                    ops.PROFILER.stop()
+                    continue
+                res.append((us, var, sp))
+        res.sort()
+        best = {}
+        for us, v, s in res:
+            best.setdefault(v, (us, s))
+        line = "  ".join(f"v{v}/s{s} {u:6.1f}us {flop / u / 1e6:5.0f}TF" for v, (u, s) in sorted(best.items()))
+        print(f"{B}x{H}x{W} {Ci}->{Co}: {line}", flush=True)
+        del xp, w, pc
+
+
+if __name__ == "__main__":
+    main()
