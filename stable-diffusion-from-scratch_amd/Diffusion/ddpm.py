@@ -42,12 +42,22 @@ class DiffusionWrapper(nn.Module):
             self._graphed = GraphedUNet(self.diffusion_model)
         self._graphs_on = bool(on)
 
+    @staticmethod
+    def _int_timesteps(t, device):
+        """Timesteps as int64 on the device, the same check on both paths: fractional values raise
+        (the UNet's sinusoidal table is indexed by integer steps); only a floating-point t is
+        checked, so the sampler's int64 timesteps never cost a host sync."""
+        if not torch.is_tensor(t):
+            t = torch.as_tensor(t)
+        if t.is_floating_point():
+            if not bool((t == t.round()).all()):
+                raise ValueError("sd_amd: timesteps must be integral")
+        return t.to(device=device, dtype=torch.long)
+
     def _unet(self, x, t, context=None):
+        t = self._int_timesteps(t, x.device)
         if self._graphs_on:
-            if not torch.is_tensor(t):
-                t = torch.as_tensor(t, device=x.device)
-            return self._graphed(x, t.to(device=x.device, dtype=torch.long).reshape(-1).expand(x.shape[0]),
-                                 context)
+            return self._graphed(x, t.reshape(-1).expand(x.shape[0]), context)
         return self.diffusion_model(x, t, context=context)
 
     def forward(self, x, t, c_concat: list = None, c_crossattn: list = None):

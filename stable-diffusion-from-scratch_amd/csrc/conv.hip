@@ -1429,6 +1429,9 @@ struct HCfg {
   static constexpr int WRING_BYTES = 2 * WSTAGE_H * 2;
   static constexpr int VEC_BYTES = 2 * TBN * 4;           // staged bias / embedding row
   static constexpr int MAX_RP = (160 * 1024 - WRING_BYTES - VEC_BYTES) / 1024;
+  static constexpr int APIECES = TBM / 8;                 // 1-KiB pieces of a shortcut (1x1 segment) A tile
+  static constexpr int APW = (APIECES + NW - 1) / NW;
+  static_assert(2 * TBM * BK * 2 <= MAX_RP * 1024, "two shortcut A tiles fit in the halo ring");
   static_assert(WRING_BYTES / NW >= EPG_BYTES + TM / 16 * TN * 8, "per-wave epilogue scratch in the W ring");
   static_assert(TBN <= NT && TBN % 8 == 0 && TM % 16 == 0 && TN % 16 == 0, "tile shape");
 };
@@ -1459,9 +1462,13 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_halo_kernel(Params p)
   int tm, tn, sidx;
   item_coords(p, it, tm, tn, sidx);
   const int m0 = tm * CF::TBM, n0 = tn * CF::TBN;
-  const int kt0 = sidx * p.kt_per_split, kt1 = min(p.kt_total, kt0 + p.kt_per_split);   // multiples of 9
+  const int kt0 = sidx * p.kt_per_split, kt1 = min(p.kt_total, kt0 + p.kt_per_split);   // kt0 % 9 == 0
+  // K-steps [0, kts1): the 3x3 segment (9 per channel block); [kts1, kt_total): the fused 1x1 shortcut
+  // over the output grid (ResBlock nin_shortcut), its A tiles staged in the idle halo ring
+  const int kts1 = p.nseg > 1 ? p.seg[1].kt_begin : p.kt_total;
   const int lrow = lane >> 3;
   const Seg& g0 = p.seg[0];
+  const Seg& g1 = p.seg[1];
   const DmaSrc d = make_dma_src(p);
   const int NP = p.h_np, RP = p.h_rp, HS = p.h_hs;
   half_t* const halo = lds + 2 * CF::WSTAGE_H;
@@ -1494,9 +1501,28 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_halo_kernel(Params p)
     for (int i = 0; i < CF::WPW; ++i)
       if (i < wcnt) ph_dma(d.w, lds + stage * CF::WSTAGE_H + (wave + CF::NW * i) * 8 * BK, wv[i], kt * BK * 2);
   };
+  // shortcut A pieces of this wave: tile rows 8 * (wave + NW * i) + lrow (row-major, swizzled like W)
+  const int acnt = wave < CF::APIECES ? (CF::APIECES - wave + CF::NW - 1) / CF::NW : 0;
+  auto issue_a1 = [&](int kt, int stage) __attribute__((always_inline)) {
+    const int c = (kt - kts1) * BK;
+    const bool second = c >= g1.c_split;
+    const unsigned ld2 = (unsigned)(second ? g1.ld1 : g1.ld0) * 2u;
+    const unsigned cc2 = (unsigned)(c - (second ? g1.c_split : 0)) * 2u;
+#pragma unroll
+    for (int i = 0; i < CF::APW; ++i) {
+      const int piece = wave + CF::NW * i;
+      if (i < acnt) {
+        const int m = m0 + piece * 8 + lrow;
+        const unsigned rch = (unsigned)((lane & 7) ^ ((4 * piece + (lrow >> 1)) & 7));
+        ph_dma(second ? d.s1 : d.s0, halo + stage * CF::TBM * BK + piece * 8 * BK,
+               m < p.M ? (unsigned)m * ld2 + rch * 16u + cc2 : PH_OOB, 0);
+      }
+    }
+    return acnt;
+  };
   // halo stream: global piece g = cb * NP + q, issued by wave (g - cb0 * NP) % NW into slot g % RP
   const int cb0 = kt0 / 9;
-  const int gend = ((kt1 + 8) / 9) * NP;
+  const int gend = kt0 < kts1 ? ((min(kt1, kts1) + 8) / 9) * NP : 0;
   int gw = cb0 * NP + wave, cbw = cb0, qw = wave, sw = gw % RP;   // this wave's next piece (NW <= NP)
   auto issue_halo = [&](int hi) __attribute__((always_inline)) {
     int n = 0;
@@ -1525,37 +1551,54 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_halo_kernel(Params p)
 #pragma unroll
     for (int j = 0; j < CF::FN16; ++j) acc16[i][j] = f4{};
   const int brow16 = wn * CF::TN + r16;
+  const int arow16 = wm * CF::TM + r16;
 
-  // prologue: W of the first K-step, the first block's early halo pieces
+  // prologue: W of the first K-step, the first block's early halo pieces (or the first shortcut tile)
   issue_w(kt0, 0);
-  issue_halo(min(gend, cb0 * NP + p.h_phi[0]));
+  if (kt0 < kts1) issue_halo(min(gend, cb0 * NP + p.h_phi[0]));
+  else issue_a1(kt0, (kt0 - kts1) & 1);
   int cb = cb0, j = 0;
   int cbslot = (cb0 * NP) % RP;   // slot of the current block's piece 0
 #if !defined(SDK_NO_PRIO)
   if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= CF::NT / 2) __builtin_amdgcn_s_setprio(1);
 #endif
   for (int kt = kt0; kt < kt1; ++kt) {
+    const bool s1 = kt >= kts1;
+    // the first shortcut K-step after the 3x3 ones: its tile goes into the ring the last 3x3 K-step
+    // was reading (free since that K-step's closing barrier) and is waited for now
+    if (kt == kts1 && kt != kt0) issue_a1(kt, 0);
     int n = 0;
     if (kt + 1 < kt1) {
       issue_w(kt + 1, (kt + 1 - kt0) & 1);
       n = wcnt;
+      if (s1) n += issue_a1(kt + 1, (kt + 1 - kts1) & 1);
     }
-    n += issue_halo(min(gend, cb * NP + p.h_phi[j + 1]));
+    if (!s1) n += issue_halo(min(gend, cb * NP + p.h_phi[j + 1]));
     vmcnt_wait_dyn(__builtin_amdgcn_readfirstlane(n));
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     const half_t* st = lds + ((kt - kt0) & 1) * CF::WSTAGE_H;
-    const int ky = j / 3, toff = ky * HS + (j - 3 * ky);
     const half_t* ab[CF::FM16];
     int sx[CF::FM16];
+    if (!s1) {
+      const int ky = j / 3, toff = ky * HS + (j - 3 * ky);
 #pragma unroll
-    for (int i = 0; i < CF::FM16; ++i) {
-      const int h = hb[i] + toff;
-      int slot = cbslot + (h >> 3);
-      slot -= slot >= RP ? RP : 0;
-      ab[i] = halo + slot * 512 + (h & 7) * 64;
-      sx[i] = (h >> 1) & 7;
+      for (int i = 0; i < CF::FM16; ++i) {
+        const int h = hb[i] + toff;
+        int slot = cbslot + (h >> 3);
+        slot -= slot >= RP ? RP : 0;
+        ab[i] = halo + slot * 512 + (h & 7) * 64;
+        sx[i] = (h >> 1) & 7;
+      }
+    } else {
+      const half_t* sa = halo + ((kt - kts1) & 1) * CF::TBM * BK;
+#pragma unroll
+      for (int i = 0; i < CF::FM16; ++i) {
+        const int r = arow16 + i * 16;
+        ab[i] = sa + r * BK;
+        sx[i] = (r >> 1) & 7;
+      }
     }
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) {
@@ -1571,9 +1614,9 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_halo_kernel(Params p)
       }
     }
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();      // everyone done reading this K-step's W stage and halo slots
+    __builtin_amdgcn_s_barrier();      // everyone done reading this K-step's W stage and A slots
     __builtin_amdgcn_sched_barrier(0);
-    if (++j == 9) {
+    if (!s1 && ++j == 9) {
       j = 0;
       ++cb;
       cbslot += NP;
@@ -2404,7 +2447,9 @@ int launch_glds(const Params& p, hipStream_t s) {
 template <class CF>
 int launch_halo(const Params& p, hipStream_t s) {
   static std::atomic<unsigned long long> attr_set{0};
-  if (p.h_rp <= 0 || p.h_rp > CF::MAX_RP || p.h_np > p.h_rp || p.kt_per_split % 9 || p.kt_total % 9)
+  const int kts1 = p.nseg > 1 ? p.seg[1].kt_begin : p.kt_total;
+  if (p.h_rp <= 0 || p.h_rp > CF::MAX_RP || p.h_np > p.h_rp || p.kt_per_split % 9 || kts1 % 9 ||
+      (p.nseg > 1 && p.h_rp * 1024 < 2 * CF::TBM * BK * 2))
     return fail(SDK_EINVAL, "conv2d: halo plan out of range");
   const int lds_bytes = CF::WRING_BYTES + p.h_rp * 1024 + CF::VEC_BYTES;
   if (int e = ensure_dyn_lds((const void*)conv_halo_kernel<CF>, 160 * 1024, attr_set, "conv2d")) return e;
@@ -2598,7 +2643,11 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   // (halo_sched.h).  Forced but not applicable: the planner's choice, as for the other variants.
   if (forced == 36 || forced == 37) {
     const sdk_conv_src& g = a->seg[0];
-    const bool shape_ok = !transform && a->nseg == 1 && g.ksize == 3 && g.stride == 1 && g.pad == 0 &&
+    // a second segment is the fused 1x1 shortcut over the output grid (transform excludes other shapes),
+    // read in whole 64-channel blocks
+    const sdk_conv_src& g1 = a->seg[1];
+    const bool seg1_ok = a->nseg == 1 || (g1.cin % BK == 0 && (g1.c_split == g1.cin || g1.c_split % BK == 0));
+    const bool shape_ok = !transform && seg1_ok && g.ksize == 3 && g.stride == 1 && g.pad == 0 &&
                           g.pad_end == 0 && !g.upsample && p.nomask && a->out_mode != SDK_OUT_GEGLU_F16;
     const int tbm = forced == 36 ? HCfg256x320::TBM : HCfg128x320::TBM;
     const int tbn = HCfg256x320::TBN;
@@ -2614,15 +2663,15 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
       p.h_np = hp.np;
       p.h_rp = hp.rp;
       for (int j = 0; j < 10; ++j) p.h_phi[j] = hp.phi[j];
-      const int ncb = kt / 9, tiles = p.tiles_m * p.tiles_n;
+      const int tiles = p.tiles_m * p.tiles_n;
       int split = a->split_k;
       if (split <= 0) {
         split = 1;
-        while (tiles * split < 256 && ncb / (split * 2) >= 2 && split < 16) split *= 2;
+        while (tiles * split < 256 && kt / (split * 2) >= 18 && split < 16) split *= 2;
       }
       if (a->cout % 8) split = 1;
-      split = std::max(1, std::min(split, ncb));
-      p.kt_per_split = 9 * ((ncb + split - 1) / split);   // splits on channel-block boundaries
+      split = std::max(1, std::min(split, (kt + 8) / 9));
+      p.kt_per_split = 9 * (((kt + split - 1) / split + 8) / 9);   // split starts on 3x3 channel-block boundaries
       split = (kt + p.kt_per_split - 1) / p.kt_per_split;
       p.split = split;
       const int64_t ws = split > 1 ? (int64_t)split * p.M * p.Npad * 4 : 0;

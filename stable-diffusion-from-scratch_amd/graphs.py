@@ -17,8 +17,13 @@ Soundness rules (each one is what a replay reads from memory it does not own):
 * re-packing the weights (``UNetModel.prepare`` after ``load_state_dict``) bumps the
   model's ``prepare_generation`` and drops every graph.
 Preconditions: run one eager step first so the conv autotuner, the workspaces and the
-context K/V cache are settled; the returned tensor is the graph's static output and is
-overwritten by the next replay (the DDIM update consumes it immediately).
+context K/V cache are settled.  The result is a fresh tensor per call, as the eager forward
+returns (a copy of the graph's static output, 1 MiB at the C3 batch: a caller may keep eps
+across calls — PLMS-style samplers, separate cond / uncond calls); ``alias_output=True`` returns
+the static buffer itself, overwritten by the next replay, for a caller that consumes it at once.
+Every new conditioning tensor (a new prompt) is a new key: one eager warm-up plus one capture,
+and each kept graph owns a private memory pool of one forward's activations, so at most
+``MAX_GRAPHS`` (4) are kept, least recently used first out.
 The reference has no counterpart (eager PyTorch, ``ldm/diffusion/ddim.py`` calls
 ``apply_model`` per step); this is the MI355X launch-overhead remedy."""
 from __future__ import annotations
@@ -29,10 +34,11 @@ import torch
 
 
 class GraphedUNet:
-    MAX_GRAPHS = 8
+    MAX_GRAPHS = 4
 
-    def __init__(self, unet):
+    def __init__(self, unet, alias_output=False):
         self.unet = unet
+        self.alias_output = alias_output
         self.graphs = OrderedDict()
         self._gen = getattr(unet, "prepare_generation", None)
 
@@ -81,7 +87,7 @@ class GraphedUNet:
         ent["x"].copy_(x)
         ent["t"].copy_(timesteps)
         ent["graph"].replay()
-        return ent["out"]
+        return ent["out"] if self.alias_output else ent["out"].clone()
 
     def reset(self):
         self.graphs.clear()

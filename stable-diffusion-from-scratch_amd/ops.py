@@ -199,7 +199,7 @@ class _Autotune:
     Enabled by ``enable()`` (UNetModel/AutoEncoderKL.prepare(autotune=True)); the
     first call of each distinct problem times every candidate (HIP events, 3 reps
     after a warm-up; SD_AMD_TUNE_REPS) and caches the fastest.  Never runs under graph capture."""
-    VARIANTS = (2, 5, 7, 6, 4, 3, 8, 9, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 31, 32, 33, 34, 35)
+    VARIANTS = (2, 5, 7, 6, 4, 3, 8, 9, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 31, 32, 33, 34, 35, 36, 37)
     SPLITS = (0, 1, 2, 4, 8)
 
     def __init__(self):
@@ -267,6 +267,8 @@ class _Autotune:
                 a.variant_hint, a.split_k = v + 1, sp
                 if lib().sdk_conv2d_plan(C.byref(a), C.byref(info)) != 0:
                     continue
+                if info.variant != v:
+                    continue             # the forced variant does not apply: the planner's pick is timed once, as its own id
                 if sp == 0 and info.split_k in self.SPLITS[1:]:
                     continue             # the automatic split equals an explicit candidate
                 part = None
@@ -309,6 +311,15 @@ FORCE_VARIANT = None
 # GroupNorm statistics emitted by the producing conv (tensor attribute; see conv2d(gn_stats=True))
 GN_ATTR = "_sd_gn_partial"
 EMIT_GN_STATS = True      # tests / A/B: False = every GroupNorm runs its own statistics pass
+
+
+def _claim(out):
+    """A caller-supplied ``out`` is about to be overwritten through the C ABI, which does not move
+    torch's version counter: drop any GroupNorm statistics a previous producer attached to it, so
+    only the plan that writes it now can attach (fresh) ones."""
+    if out is not None and hasattr(out, GN_ATTR):
+        delattr(out, GN_ATTR)
+    return out
 
 
 # The LDS-DMA conv kernels address a source through a buffer resource (31-bit byte offsets); a source
@@ -366,6 +377,7 @@ def conv2d(pc: PackedConv, x, *, ksize=None, stride=1, pad=None, pad_end=0, upsa
     or autotuner).  ``gn_stats``: the output feeds a GroupNorm — when the chosen plan can, the
     epilogue also emits its per-chunk channel statistics (attached to the returned tensor,
     consumed by ``group_norm``, which then skips its statistics pass)."""
+    _claim(out)
     B0 = _as_pair(x)[0].shape[0]
     if B0 > 1 and (_src_bytes(x) >= BUF_LIMIT or (seg2 is not None and _src_bytes(seg2[0]) >= BUF_LIMIT)):
         if out is None:
@@ -463,6 +475,7 @@ def linear(pc: PackedConv, x2d, *, silu=False, residual=None, out_mode=OUT_NHWC_
            act=ACT_NONE):
     """Token GEMM: x2d [M, K] fp16 → [M, N]; a 1x1 conv over an M x 1 image.  ``silu`` applies to
     the input (prologue), ``act`` to the output (epilogue, before the residual)."""
+    _claim(out)
     M = x2d.shape[0]
     x4 = x2d.view(1, M, 1, x2d.shape[-1]) if x2d.stride(-1) == 1 and x2d.is_contiguous() else None
     if x4 is None:
@@ -504,7 +517,8 @@ def group_norm_apply(x, gn, silu=True, out=None, pad=0):
     ``pad`` > 0 writes it into a zero-bordered [B, H+2pad, W+2pad, C] image for a pad-0 3x3 conv."""
     args, (B, H, W, Ch), dev = _gn_args(x)
     args.scale, args.shift = gn[0].data_ptr(), gn[1].data_ptr()
-    y = out if out is not None else torch.empty(B, H + 2 * pad, W + 2 * pad, Ch, dtype=torch.float16, device=dev)
+    y = _claim(out) if out is not None else torch.empty(B, H + 2 * pad, W + 2 * pad, Ch, dtype=torch.float16,
+                                                          device=dev)
     if PROFILER.active:
         PROFILER.begin("gn_apply", None)
     if pad:
@@ -605,7 +619,8 @@ def group_norm(x, gamma, beta, eps, groups=32, silu=True, pad=0, out=None):
     args.scale, args.shift = scale.data_ptr(), shift.data_ptr()
     ws = WORKSPACE.get(lib().sdk_group_norm_workspace(B, H * W, Ch), dev)
     args.workspace, args.workspace_bytes = ws.data_ptr(), ws.numel()
-    y = out if out is not None else torch.empty(B, H + 2 * pad, W + 2 * pad, Ch, dtype=torch.float16, device=dev)
+    y = _claim(out) if out is not None else torch.empty(B, H + 2 * pad, W + 2 * pad, Ch, dtype=torch.float16,
+                                                          device=dev)
     # statistics the producing convs emitted (every source must carry them)
     srcs = [t for t in _as_pair(x) if t is not None]
     parts = [getattr(t, GN_ATTR, None) for t in srcs]
@@ -628,7 +643,7 @@ def group_norm(x, gamma, beta, eps, groups=32, silu=True, pad=0, out=None):
 def layer_norm(x2d, gamma, beta, eps=1e-5, out=None):
     _need_cuda(x2d, "layer_norm")
     M, Cc = x2d.shape
-    y = out if out is not None else torch.empty(M, Cc, dtype=torch.float16, device=x2d.device)
+    y = _claim(out) if out is not None else torch.empty(M, Cc, dtype=torch.float16, device=x2d.device)
     if PROFILER.active:
         PROFILER.begin("layer_norm", None)
     check(lib().sdk_layer_norm(_ptr(x2d), _ptr(y), M, Cc, x2d.stride(0), y.stride(0), _ptr(gamma), _ptr(beta),
@@ -687,6 +702,7 @@ def attention(q, k, v, *, batch, heads, nq, nk, head_dim, scale, out=None, causa
         _need_cuda(t, "attention " + n)
     if out is None:
         out = torch.empty(batch * nq, heads * head_dim, dtype=torch.float16, device=q.device)
+    _claim(out)
     a = AttentionArgs()
     a.q, a.k, a.v, a.o = q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr()
     a.q_ld, a.k_ld, a.v_ld, a.o_ld = q.stride(0), k.stride(0), v.stride(0), out.stride(0)
@@ -720,6 +736,8 @@ def cross_attention_block(t, kv, pc_q: PackedConv, pc_o: PackedConv, *, batch, n
         raise ValueError("sd_amd.cross_attention_block: to_q / to_out must be channels x channels")
     if out is None:
         out = torch.empty(batch * n_img, Cc, dtype=torch.float16, device=t.device)
+    _claim(out)
+    _claim(out_ln)
     a = XAttnArgs()
     a.t, a.kv, a.wq, a.wo = t.data_ptr(), kv.data_ptr(), pc_q.weight.data_ptr(), pc_o.weight.data_ptr()
     a.bias = pc_o.bias.data_ptr() if pc_o.bias is not None else None

@@ -108,3 +108,36 @@ def test_halo_concat_rowbias_residual_gn_stats(ops, variant):
     pp, nch, _ = getattr(y, ops.GN_ATTR)
     pt, ncht, _ = getattr(yt, ops.GN_ATTR)
     assert nch == ncht and torch.equal(pp, pt)
+
+
+@pytest.mark.parametrize("variant", [36, 37])
+@pytest.mark.parametrize("B,H,W,C0,C1,C2,Co,split", [
+    (2, 32, 32, 320, 320, 320, 320, 1),      # decoder ResBlock conv2 + 1x1 over the concat input
+    (2, 16, 16, 640, 640, 320, 640, 1),
+    (1, 16, 16, 640, 1280, 0, 640, 3),       # split-K: splits start in the 3x3 and in the 1x1 segment
+    (3, 8, 8, 128, 192, 64, 320, 2),         # multi-image tiles
+])
+def test_halo_fused_shortcut_segment(ops, variant, B, H, W, C0, C1, C2, Co, split):
+    """ResBlock conv2 with the nin_shortcut folded in as a second K segment (a plain 1x1 over the raw,
+    possibly concatenated block input): its A tiles are staged in the idle halo ring after the 3x3 K-steps."""
+    h = _rand(B, H, W, C0, seed=21)
+    a = _rand(B, H, W, C1, seed=22)
+    c = _rand(B, H, W, C2, seed=23) if C2 else None
+    g = torch.Generator().manual_seed(24)
+    w2 = torch.randn(Co, C0, 3, 3, generator=g) / math.sqrt(C0 * 9)
+    ws = torch.randn(Co, C1 + C2, 1, 1, generator=g) / math.sqrt(C1 + C2)
+    b = torch.randn(Co, generator=g) * 0.1
+    res_src = (a.to(DEV), c.to(DEV)) if C2 else a.to(DEV)
+    pc = ops.PackedConv([(w2, C0), (ws, C1 + C2)], b, device=DEV)
+    hp = _padded(h).to(DEV)
+    y, ran = _ran(ops, lambda: ops.conv2d(pc, hp, pad=0, seg2=(res_src, None, False), variant=variant, split_k=split))
+    if ran != variant:
+        assert (variant, H) == (36, 8), "the halo plan should exist for this shape"
+        pytest.skip("4 images per 256-pixel tile overflow the ring: the planner runs")
+    xin = torch.cat([a, c], -1) if C2 else a
+    ref = (F.conv2d(h.float().permute(0, 3, 1, 2), w2.half().float(), b, padding=1) +
+           F.conv2d(xin.float().permute(0, 3, 1, 2), ws.half().float())).permute(0, 2, 3, 1)
+    assert rel_l2(y, ref) < 2e-3
+    if split == 1:
+        yt = ops.conv2d(pc, hp, pad=0, seg2=(res_src, None, False), variant=TWIN[variant], split_k=1)
+        assert torch.equal(y, yt)

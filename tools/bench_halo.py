@@ -10,7 +10,14 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from tools.sweep_shape import graph_us  # noqa: E402
 
-SHAPES = [  # B, H, W, Cin, Cout (3x3, stride 1)
+SHAPES = [  # B, H, W, Cin, Cout (3x3, stride 1)[, Cskip: fused 1x1 shortcut segment over a raw input]
+    (16, 64, 64, 320, 320, 640),
+    (16, 32, 32, 640, 640, 1920),
+    (16, 32, 32, 640, 640, 320),
+    (16, 16, 16, 1280, 1280, 2560),
+    (16, 8, 8, 1280, 1280),
+    (16, 8, 8, 2560, 1280),
+    (16, 8, 8, 1280, 1280, 2560),
     (16, 64, 64, 320, 320),
     (16, 64, 64, 640, 320),
     (16, 64, 64, 960, 320),
@@ -32,16 +39,21 @@ def main():
     from sd_amd import ops
     variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "22,23,5,8,20,36,37").split(",")]
     splits = [int(v) for v in (sys.argv[2] if len(sys.argv) > 2 else "1,2,4,8").split(",")]
-    for B, H, W, Ci, Co in SHAPES:
+    for B, H, W, Ci, Co, *sk in SHAPES:
         torch.manual_seed(0)
         xp = torch.randn(B, H + 2, W + 2, Ci, device="cuda").half()
         w = torch.randn(Co, Ci, 3, 3, device="cuda") / (Ci * 9) ** 0.5
-        pc = ops.PackedConv([(w, Ci)], torch.zeros(Co, device="cuda"), device="cuda")
-        flop = 2.0 * B * H * W * Co * Ci * 9
+        segs = [(w, Ci)]
+        seg2 = None
+        if sk:
+            segs.append((torch.randn(Co, sk[0], 1, 1, device="cuda") / sk[0] ** 0.5, sk[0]))
+            seg2 = (torch.randn(B, H, W, sk[0], device="cuda").half(), None, False)
+        pc = ops.PackedConv(segs, torch.zeros(Co, device="cuda"), device="cuda")
+        flop = 2.0 * B * H * W * Co * (Ci * 9 + (sk[0] if sk else 0))
         res = []
         for var in variants:
             for sp in splits:
-                f = lambda: ops.conv2d(pc, xp, pad=0, variant=var, split_k=sp)   # noqa: E731
+                f = lambda: ops.conv2d(pc, xp, pad=0, seg2=seg2, variant=var, split_k=sp)   # noqa: E731
                 try:
                     ops.PROFILER.start()
                     f()
@@ -59,7 +71,7 @@ def main():
         for us, v, s in res:
             best.setdefault(v, (us, s))
         line = "  ".join(f"v{v}/s{s} {u:6.1f}us {flop / u / 1e6:5.0f}TF" for v, (u, s) in sorted(best.items()))
-        print(f"{B}x{H}x{W} {Ci}->{Co}: {line}", flush=True)
+        print(f"{B}x{H}x{W} {Ci}->{Co}{'+' + str(sk[0]) if sk else ''}: {line}", flush=True)
         del xp, w, pc
 
 
