@@ -150,6 +150,21 @@ def rank_inputs(seed, world, rank, batch, latent_shape, ctx_shape, device):
     return xT, ctx
 
 
+# The reference itself timed as written on the survey container's CPU (BASELINE.md:22-25):
+# not re-run here (/root/reference does not exist on the GPU box), carried beside the port's figure
+REFERENCE_AS_WRITTEN = {
+    "c3": {"value": 0.00516, "unit": "images/sec", "cores": 8, "kind": "reference",
+           "sample": "reference path as written, B=1 full 50-step run + decode, 193.8 s/img, 8-vCPU Xeon "
+                     "(survey container, BASELINE.md:22)"},
+    "c2": {"value": 0.0466, "unit": "images/sec", "cores": 8, "kind": "reference",
+           "sample": "reference path as written, B=8 UNet step 3.22 s + decode 10.3 s, extrapolated to 50 steps, "
+                     "8-vCPU Xeon (BASELINE.md:24)"},
+    "c5": {"value": 0.00273, "unit": "images/sec", "cores": 8, "kind": "reference",
+           "sample": "reference path as written (eps-pred), B=8 UNet step 56.9 s + decode 90.3 s, extrapolated, "
+                     "8-vCPU Xeon (BASELINE.md:25)"},
+}
+
+
 def unet_gflops_per_image(cfg):
     return {"c3": 803.3, "c2": 125.1, "c5": 2149.1, "c1": 3.275}[cfg]
 
@@ -304,21 +319,29 @@ def _free_port():
     return port
 
 
-def launch_ranks(n):
+def launch_ranks(n, entry=None):
     """``bench.py --gpus N`` (N > 1) started without a launcher: this GPU-free parent checks that N
     devices are visible (device_count does not initialise the GPU on this image) and starts one
-    rank per GPU with torch.distributed.run as a CHILD process (no exec), exiting with its code."""
+    rank per GPU with torch.distributed.run as a CHILD process (no exec), exiting with its code.
+    ``entry``: the per-rank script (default this file; tests/bench_rank_stub.py in the CPU rehearsal)."""
     import subprocess
     have = torch.cuda.device_count()
-    if have < n:
+    if have < n and not _rehearsal():
         print(f"bench.py: --gpus {n} needs {n} visible GPUs, found {have}; refusing to report a "
               f"{have}-GPU number as an {n}-GPU one", file=sys.stderr, flush=True)
         sys.exit(3)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}",
+           os.path.abspath(entry or __file__)] + sys.argv[1:]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     sys.exit(subprocess.call(cmd, env=env))
+
+
+def _rehearsal():
+    """SD_AMD_BENCH_REHEARSAL=cpu: the launcher and rank plumbing on the CPU (gloo, no GPU) — the
+    tests' rehearsal of the 8-GPU launch; never set for a measured run."""
+    return os.environ.get("SD_AMD_BENCH_REHEARSAL") == "cpu"
 
 
 def setup_ranks(args):
@@ -334,11 +357,17 @@ def setup_ranks(args):
     if world != args.gpus:
         print(f"bench.py: launched with WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr, flush=True)
         sys.exit(3)
+    dist = world > 1
+    if _rehearsal():
+        if dist:
+            import torch.distributed as tdist
+            tdist.init_process_group("gloo")
+            assert tdist.get_world_size() == args.gpus
+        return world, rank, local, dist, torch.device("cpu")
     if torch.cuda.device_count() <= local:
         print(f"bench.py: rank {rank} has no GPU of its own (local rank {local}, "
               f"{torch.cuda.device_count()} visible)", file=sys.stderr, flush=True)
         sys.exit(3)
-    dist = world > 1
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     if dist:
@@ -348,7 +377,7 @@ def setup_ranks(args):
     return world, rank, local, dist, device
 
 
-def main():
+def make_parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
@@ -364,7 +393,11 @@ def main():
                     help="conv tile/split-K table measured on MI355X (loaded if present; missing problems are timed)")
     ap.add_argument("--tuning-out", default=None, help="write the (extended) tuning table here")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one HIP graph per UNet step")
-    args = ap.parse_args()
+    return ap
+
+
+def main():
+    args = make_parser().parse_args()
 
     world, rank, local, dist, device = setup_ranks(args)
     cfg = CONFIGS[args.config]
@@ -502,6 +535,8 @@ def main():
         out["end_to_end_tflops"] = round(tot_tf * value, 1)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.config, cfg, args.ddim_steps, args.cpu_threads)
+        if args.config in REFERENCE_AS_WRITTEN:
+            out["cpu_baseline"]["reference_as_written"] = REFERENCE_AS_WRITTEN[args.config]
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

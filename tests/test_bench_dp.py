@@ -118,3 +118,44 @@ def test_bench_rejects_world_size_mismatch():
     assert r.returncode != 0
     assert "WORLD_SIZE=2 but --gpus 4" in r.stderr
     assert '"metric"' not in r.stdout
+
+
+def _launch(n, tmp_path, extra_env=None):
+    """bench.launch_ranks(n) as bench.py --gpus n runs it (GPU-free parent -> torch.distributed.run child
+    -> one process per rank), with tests/bench_rank_stub.py as the rank entry, in a subprocess (the
+    launcher ends with sys.exit(child status))."""
+    out = str(tmp_path / "stub.pt")
+    code = ("import sys, torch; sys.path.insert(0, %r); import bench; "
+            "sys.argv = ['bench.py', '--gpus', '%d', '--steps', '2', '--warmup', '1', '--ddim-steps', '4']; "
+            "torch.cuda.device_count = lambda: %d; "
+            "bench.launch_ranks(%d, entry=%r)") % (ROOT, n, n, n, os.path.join(ROOT, "tests", "bench_rank_stub.py"))
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(SD_AMD_BENCH_REHEARSAL="cpu", BENCH_STUB_OUT=out, OMP_NUM_THREADS="1", **(extra_env or {}))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=300, cwd=ROOT)
+    return r, out
+
+
+def test_launch_ranks_spawns_ranks_and_gathers_rank_major(tmp_path):
+    """bench.launch_ranks(2) on the CPU: two ranks with RANK / LOCAL_RANK / WORLD_SIZE = (r, r, 2) from
+    torch.distributed.run, bench.setup_ranks agreeing with them, and the all-gathered batch in rank-major
+    order equal to the single-process result bit for bit."""
+    r, out = _launch(2, tmp_path)
+    assert r.returncode == 0, r.stdout + r.stderr
+    res = torch.load(out, weights_only=True)
+    plumb = res["plumbing"].tolist()
+    assert plumb == [[0, 0, 2, 0, 0], [1, 1, 2, 1, 1]]
+    import bench
+    xg, cg = bench.rank_inputs(2024, 1, 0, 2 * 3, (4, 8, 8), (5, 16), torch.device("cpu"))
+    z, _ = _StubSampler().sample(4, 2 * 3, (4, 8, 8), conditioning=cg, x_T=xg)
+    assert torch.equal(res["gathered"], _StubLD().decode_first_stage(z).half())
+    assert res["elapsed"] > 0
+
+
+def test_launch_ranks_propagates_a_failing_rank(tmp_path):
+    """A rank that dies (status 7) fails the whole launch: the launcher's caller exits non-zero and no
+    bench line is printed."""
+    r, _ = _launch(2, tmp_path, {"BENCH_STUB_FAIL_RANK": "1"})
+    assert r.returncode != 0
+    assert '"metric"' not in r.stdout

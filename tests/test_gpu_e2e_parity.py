@@ -1,0 +1,123 @@
+"""End-to-end parity of the benchmarked configurations vs the fp32 CPU oracle chain (run with -m gpu).
+
+* C3 (the headline): the bench's own ``one_step`` — B = 16, the committed conv tuning table, HIP-graph
+  replay, 50 DDIM steps through LatentDiffusion.apply_model, then the 64² → 512² decode — and image 0
+  of it against ``oracle.sampler_ref.ddim_sample`` → ``oracle.unet_ref.unet_forward`` (50 fp32 UNet
+  evaluations) → ``oracle.vae_ref.decode_first_stage`` on the same seeded weights and inputs.
+  Reference path: ``ldm/diffusion/ddim.py:114-206`` (sampling loop), ``ldm/diffusion/ddpm.py:1095``
+  (decode_first_stage).
+* C2 (uncond 256², B = 8): the same 50-step chain on samples 0 and 7 of the bench batch.
+* C5 (SD-2 shape 768², v-prediction, B = 8): one UNet evaluation at the bench batch (tuning table,
+  graph replay) on samples 0 and 7, and the B = 8 decode of images 0 and 7 — a 50-step fp32 chain at
+  96² would take ~6 min of CPU.
+Every comparison prints and asserts rel-L2 AND max-abs error (relative to the oracle's max-abs); the
+thresholds are ~3x the errors measured on MI355X (profiles/r3_parity_errors.txt)."""
+import os
+import sys
+import time
+
+import pytest
+import torch
+
+from gpu_util import rel_l2
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+THREADS = 16
+
+
+def max_abs_rel(a, b):
+    """max |a - b| over max |b| (the oracle's range)."""
+    a, b = a.detach().float().cpu(), b.detach().float().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+def _report(tag, got, ref, rl2_max, mabs_max):
+    rl2, mab = rel_l2(got, ref), max_abs_rel(got, ref)
+    print(f"[parity] {tag}: rel-L2 {rl2:.3e} (<= {rl2_max:.0e})  max-abs/max {mab:.3e} (<= {mabs_max:.0e})",
+          flush=True)
+    assert rl2 <= rl2_max, f"{tag}: rel-L2 {rl2:.3e}"
+    assert mab <= mabs_max, f"{tag}: max-abs {mab:.3e}"
+
+
+def _bench_models(name):
+    sys.path.insert(0, ROOT)
+    import bench
+    from sd_amd import ops
+    cfg = bench.CONFIGS[name]
+    ops.AUTOTUNE.table.clear()
+    loaded = ops.AUTOTUNE.load(os.path.join(ROOT, "configs", "conv_tuning_mi355x.json"))
+    assert loaded > 0, "the committed tuning table is stale for csrc/conv.hip"
+    ops.AUTOTUNE.enable(False)
+    unet, vae, ld = bench.build_models(cfg, DEV, graph=True)
+    B, L = cfg["batch"], cfg["latent"]
+    xT, ctx = bench.rank_inputs(2024, 1, 0, B, (4, L, L), cfg["ctx"], DEV)
+    return bench, cfg, unet, vae, ld, xT, ctx
+
+
+def _oracle_chain(cfg, usd, vsd, x_T, ctx, scale_factor, v=False):
+    from oracle.sampler_ref import ddim_sample
+    from oracle.unet_ref import unet_forward
+    from oracle.vae_ref import decode_first_stage
+    import bench
+    torch.set_num_threads(THREADS)
+    fn = lambda x, t: unet_forward(usd, cfg["unet"], x, t, ctx)   # noqa: E731
+    z, _ = ddim_sample(fn, x_T, 50, 0.0, parameterization="v" if v else "eps")
+    return decode_first_stage(vsd, bench.SD_VAE, z, scale_factor), z
+
+
+def _cpu_sd(m):
+    return {k: v.detach().float().cpu() for k, v in m.state_dict().items()}
+
+
+def test_c3_bench_step_vs_oracle_chain(sdk):
+    """The exact C3 bench step (B=16, tuning table, graphs, 50 DDIM steps + decode) — image 0 vs the
+    fp32 oracle chain (~2.5 min of CPU at 16 threads)."""
+    from sd_amd.DDIM.ddim import DDIMSampler
+    bench, cfg, unet, vae, ld, xT, ctx = _bench_models("c3")
+    assert xT.shape[0] == 16
+    ld.use_graphs(True)
+    step = bench.make_one_step(DDIMSampler(ld), ld, xT, ctx, 50, 1, None)
+    img = step().float().cpu()
+    assert img.shape == (16, 3, 512, 512) and torch.isfinite(img).all()
+    t0 = time.time()
+    ref, _ = _oracle_chain(cfg, _cpu_sd(unet), _cpu_sd(vae), xT[0:1].cpu(), ctx[0:1].cpu(), ld.scale_factor)
+    print(f"[parity] C3 oracle chain: {time.time() - t0:.0f} s", flush=True)
+    _report("C3 image 0 (50 DDIM steps + decode, B=16 bench step)", img[0:1], ref, 5e-3, 2e-2)
+
+
+def test_c2_bench_batch_vs_oracle_chain(sdk):
+    """C2 (unconditional 256², B=8): 50 DDIM steps + decode through the bench's step, samples 0 and 7."""
+    from sd_amd.DDIM.ddim import DDIMSampler
+    bench, cfg, unet, vae, ld, xT, ctx = _bench_models("c2")
+    assert xT.shape[0] == 8 and ctx is None
+    ld.use_graphs(True)
+    step = bench.make_one_step(DDIMSampler(ld), ld, xT, ctx, 50, 1, None)
+    img = step().float().cpu()
+    usd, vsd = _cpu_sd(unet), _cpu_sd(vae)
+    for i in (0, 7):
+        ref, _ = _oracle_chain(cfg, usd, vsd, xT[i:i + 1].cpu(), None, ld.scale_factor)
+        _report(f"C2 image {i} (50 DDIM steps + decode, B=8 bench step)", img[i:i + 1], ref, 5e-3, 2e-2)
+
+
+def test_c5_bench_batch_unet_and_decode_vs_oracle(sdk):
+    """C5 (SD-2 shape, 96² latent, v-prediction, B=8): the UNet at the bench batch with the tuning table
+    and graph replay, and the B=8 decode, samples 0 and 7 vs the fp32 oracle."""
+    from oracle.unet_ref import unet_forward
+    from oracle.vae_ref import decode_first_stage
+    bench, cfg, unet, vae, ld, xT, ctx = _bench_models("c5")
+    assert xT.shape[0] == 8
+    t = torch.full((8,), 641, dtype=torch.long, device=DEV)
+    ld.use_graphs(True)
+    ld.apply_model(xT, t, ctx)                               # capture
+    y = ld.apply_model(xT, t, ctx).float().cpu()
+    z = torch.randn(8, 4, 96, 96, generator=torch.Generator().manual_seed(31)).to(DEV)
+    dec = ld.decode_first_stage(z).float().cpu()
+    usd, vsd = _cpu_sd(unet), _cpu_sd(vae)
+    torch.set_num_threads(THREADS)
+    for i in (0, 7):
+        ref = unet_forward(usd, cfg["unet"], xT[i:i + 1].cpu(), torch.tensor([641]), ctx[i:i + 1].cpu())
+        _report(f"C5 UNet sample {i} (B=8 bench batch, graph)", y[i:i + 1], ref, 5e-3, 2e-2)
+        dref = decode_first_stage(vsd, bench.SD_VAE, z[i:i + 1].cpu(), ld.scale_factor)
+        _report(f"C5 decode image {i} (B=8 96->768)", dec[i:i + 1], dref, 5e-3, 2e-2)
