@@ -3,7 +3,8 @@
 
 * C5 (BASELINE configs[4]): the SD-2-shape UNet (``num_head_channels: 64``, context 1024,
   ``openai_model/model.py:289-315``) at a 96x96 latent — 9,216-token self-attention at d = 64 —
-  and the 96² → 768² VAE decode, each at B = 1 vs the fp32 CPU oracle (rel-L2 ≤ 2e-2).
+  and the 96² → 768² VAE decode, each at B = 1 vs the fp32 CPU oracle (rel-L2 <= 5e-3, max-abs <= 2e-2 of
+  the range).
 * v-prediction is an extension (the reference has eps / x0 only, ``Diffusion/ddpm.py:131``;
   SURVEY Q9): ε = √ᾱ·v + √(1-ᾱ)·x inside the fused DDIM update, bit-exact vs the oracle's
   restatement ``oracle.schedule.v_to_eps`` — PARITY UNPINNED (no reference value exists).
@@ -20,7 +21,7 @@ import pytest
 import torch
 
 from golden_util import cfg_of, load, weights_of
-from gpu_util import rel_l2
+from gpu_util import check_parity, rel_l2
 from synth import synth_weights
 
 pytestmark = pytest.mark.gpu
@@ -57,10 +58,8 @@ def test_c5_sd2_unet_96_latent_vs_oracle(sdk):
     y = m(x.to(DEV), t.to(DEV), ctx.to(DEV))
     torch.set_num_threads(16)
     ref = unet_forward(sd, SD2, x, t, ctx)
-    err = rel_l2(y, ref)
-    print(f"SD2 96x96 rel-L2 {err:.3e}")
     assert y.shape == (1, 4, 96, 96)
-    assert err < 2e-2
+    check_parity("C5 SD-2 UNet 96x96", y, ref)
 
 
 def test_c5_vae_decode_96_to_768_vs_oracle(sdk):
@@ -73,10 +72,8 @@ def test_c5_vae_decode_96_to_768_vs_oracle(sdk):
     dec = vae.decode(z.to(DEV), pre_scale=1.0 / 0.18215)
     torch.set_num_threads(16)
     ref = decode_first_stage(sd, SD_VAE, z, 0.18215)
-    err = rel_l2(dec, ref)
-    print(f"VAE 768 rel-L2 {err:.3e}")
     assert dec.shape == (1, 3, 768, 768)
-    assert err < 2e-2
+    check_parity("C5 VAE decode 96->768", dec, ref)
 
 
 @pytest.mark.parametrize("index", [0, 7, 25, 49])

@@ -1,7 +1,9 @@
 """Model-level parity on the MI355X (run with -m gpu): the HIP-backed mirrors against
 (a) the reference's own outputs (golden fixtures) at tiny sizes and (b) the CPU
 oracle at the real SD-1.x / VAE shapes.  Tolerance: fp16 activations, fp32
-accumulation and softmax → rel-L2 ≤ 2e-2 end to end (stated per test)."""
+accumulation and softmax; full-size models vs the fp32 oracle: rel-L2 <= 5e-3 and max-abs <= 2e-2 of the
+range (gpu_util.check_parity, ~3x the measured errors); tiny models vs the reference's golden outputs as
+stated per test."""
 import json
 
 import numpy as np
@@ -9,7 +11,7 @@ import pytest
 import torch
 
 from golden_util import cfg_of, load, weights_of
-from gpu_util import rel_l2
+from gpu_util import check_parity, rel_l2
 from synth import synth_weights
 
 pytestmark = pytest.mark.gpu
@@ -95,9 +97,7 @@ def test_full_unet_vs_oracle(sdk, cfg_name, hw, ctx_dim):
     y = m(x.to(DEV), t.to(DEV), ctx.to(DEV) if ctx is not None else None)
     torch.set_num_threads(16)
     ref = unet_forward(sd, cfg, x, t, ctx)
-    err = rel_l2(y, ref)
-    print(f"{cfg_name} rel-L2 {err:.3e}")
-    assert err < 2e-2
+    check_parity(f"{cfg_name} full UNet", y, ref)
 
 
 def test_full_vae_decode_vs_oracle(sdk):
@@ -117,9 +117,7 @@ def test_full_vae_decode_vs_oracle(sdk):
     dec = vae.decode(z.to(DEV), pre_scale=1.0 / 0.18215)
     torch.set_num_threads(16)
     ref = decode_first_stage(sd, dd, z, 0.18215)
-    err = rel_l2(dec, ref)
-    print(f"VAE rel-L2 {err:.3e}")
-    assert err < 2e-2
+    check_parity("VAE decoder 64->512", dec, ref)
 
 
 # ---------------------------------------------------------------- img2img
@@ -228,10 +226,8 @@ def test_full_vae_encode_vs_oracle(sdk):
     post = vae.encode(x.to(DEV))
     torch.set_num_threads(16)
     ref = autoencoder_moments(sd, dd, x)
-    err = rel_l2(post.parameters, ref)
-    print(f"VAE encode rel-L2 {err:.3e}")
     assert post.parameters.shape == (1, 8, 64, 64)
-    assert err < 2e-2
+    check_parity("VAE encoder 512->64 moments", post.parameters, ref)
 
 
 # ---------------------------------------------------------------- CLIP text encoder
@@ -263,10 +259,8 @@ def test_full_clip_vit_l14_vs_oracle(sdk):
     ids[0, 12:] = 49407
     y = m(ids)
     ref = clip_text_forward(sd, ids, 12)
-    err = rel_l2(y, ref)
-    print(f"CLIP ViT-L/14 rel-L2 {err:.3e}")
     assert y.shape == (2, 77, 768)
-    assert err < 2e-2
+    check_parity("CLIP ViT-L/14 text tower", y, ref)
 
 
 # ---------------------------------------------------------------- tiled decode
