@@ -165,6 +165,14 @@ int sdk_group_norm(const sdk_group_norm_args* a, int32_t silu, void* y, int32_t 
                    int32_t pad, const float* part0, int32_t nch0, const float* part1, int32_t nch1,
                    sdk_stream_t stream);
 
+/* The statistics half of sdk_group_norm alone: a->scale / a->shift [batch][channels] of the
+ * GroupNorm affine, merged from the producers' per-chunk statistics (part0 / part1 as above) or, with
+ * none, computed from x (sdk_group_norm_affine).  For a 3x3 conv that applies GroupNorm + SiLU to its
+ * own A operand (sdk_conv_src.gn_scale / gn_shift / silu with pad 1: the halo-tile conv, variants
+ * 36 / 37), so the normalised tensor is never written. */
+int sdk_group_norm_finalize(const sdk_group_norm_args* a, const float* part0, int32_t nch0, const float* part1,
+                            int32_t nch1, sdk_stream_t stream);
+
 /* The post-activation GroupNorm of the DDPM (config C1) UNet (DDPM/models/layers.py:23-38 ConvBlock,
  * :311-338 ResNetBlock, :154 attention post-norm): y = [silu](x*scale + shift) + post_bias[b][c]
  * (the time embedding added after block1) + residual[pix][c] (the ResNet skip); both optional. */

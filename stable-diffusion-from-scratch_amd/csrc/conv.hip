@@ -72,6 +72,10 @@ struct Params {
   // block, ring slots, issue schedule
   int h_hs, h_np, h_rp;
   int h_phi[10];
+  // GroupNorm-fused form (h_virt = 1): seg 0 is the RAW input with pad 1 (zero border virtual), its
+  // GroupNorm scale / shift (seg[0].gscale / gshift, [batch][cin]) and SiLU applied to each staged piece
+  // in LDS; halo row of pixel h = (h * h_divm) >> 20 (exact for the plan's pixel range)
+  int h_virt, h_divm;
 };
 
 // epilogue activation (CLIP's quick_gelu x*sigmoid(1.702x), transformers activations.py QuickGELUActivation)
@@ -1428,7 +1432,8 @@ struct HCfg {
   static constexpr int WSTAGE_H = TBN * BK;               // halfs per W stage
   static constexpr int WRING_BYTES = 2 * WSTAGE_H * 2;
   static constexpr int VEC_BYTES = 2 * TBN * 4;           // staged bias / embedding row
-  static constexpr int MAX_RP = (160 * 1024 - WRING_BYTES - VEC_BYTES) / 1024;
+  static constexpr int GNB_BYTES = 3 * 128 * 4;           // GroupNorm scale | shift of 3 channel blocks
+  static constexpr int MAX_RP = (160 * 1024 - WRING_BYTES - VEC_BYTES - GNB_BYTES) / 1024;
   static constexpr int APIECES = TBM / 8;                 // 1-KiB pieces of a shortcut (1x1 segment) A tile
   static constexpr int APW = (APIECES + NW - 1) / NW;
   static_assert(2 * TBM * BK * 2 <= MAX_RP * 1024, "two shortcut A tiles fit in the halo ring");
@@ -1451,7 +1456,12 @@ __device__ __forceinline__ void vmcnt_wait_dyn(int n) {
   }
 }
 
-template <class CF>
+// VIRT: the GroupNorm-fused form — halo pieces are DMA'd from the raw (unpadded) input, out-of-image
+// pixels read zeros, and the K-step after a piece lands its wave applies x * scale + shift (+ SiLU) to it
+// in LDS and re-zeroes the border (the same arithmetic as gn_apply_pad_kernel, so the conv equals the
+// one over the materialised zero-bordered GN output bit for bit).  The scale / shift of a channel block
+// arrive by LDS-DMA with its first piece (3-block ring).  Single-image tiles only (one scale row).
+template <class CF, bool VIRT>
 __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_halo_kernel(Params p) {
   extern __shared__ __attribute__((aligned(16))) half_t lds[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1473,10 +1483,21 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_halo_kernel(Params p)
   const int NP = p.h_np, RP = p.h_rp, HS = p.h_hs;
   half_t* const halo = lds + 2 * CF::WSTAGE_H;
   // the tile's halo: whole padded rows from the first output row it touches (whole images when a
-  // tile holds several)
+  // tile holds several); VIRT: rows of the virtually padded image (row 0 / col 0 = the zero border)
   const int b0 = m0 / p.hw_out;
   const int oy0 = (m0 - b0 * p.hw_out) / p.wo;
   const int hstart = (b0 * g0.h + oy0) * g0.w;
+  const int HROWS = VIRT ? g0.h + 2 : g0.h;               // padded rows per image
+  float* const gnb = reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + CF::WRING_BYTES + RP * 1024 +
+                                              CF::VEC_BYTES);
+  // VIRT: raw source offset (bytes, or PH_OOB for the zero border) of halo pixel h, channel offset cc2
+  auto virt_src = [&](int h, unsigned ld2, unsigned cc2) __attribute__((always_inline)) {
+    const int hr = (int)(((unsigned)h * (unsigned)p.h_divm) >> 20);
+    const int hc = h - hr * HS;
+    const int r = oy0 + hr - 1, c = hc - 1;
+    const bool in = (unsigned)r < (unsigned)g0.h && (unsigned)c < (unsigned)g0.w;
+    return in ? (unsigned)((b0 * g0.h + r) * g0.w + c) * ld2 + cc2 : PH_OOB;
+  };
   const int r16 = lane & 15, c16 = lane >> 4;
   // halo pixel of each A fragment row (tap (0, 0)); rows past M read a valid pixel, never stored
   int hb[CF::FM16];
@@ -1485,7 +1506,7 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_halo_kernel(Params p)
     const int m = min(m0 + wm * CF::TM + i * 16 + r16, p.M - 1);
     const int b = m / p.hw_out, rem = m - b * p.hw_out;
     const int oy = rem / p.wo, ox = rem - oy * p.wo;
-    hb[i] = ((b - b0) * g0.h + oy - oy0) * HS + ox;
+    hb[i] = ((b - b0) * HROWS + oy - oy0) * HS + ox;
   }
   // W pieces of this wave: tile rows 8 * (wave + NW * i) + lrow
   unsigned wv[CF::WPW];
@@ -1524,6 +1545,8 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_halo_kernel(Params p)
   const int cb0 = kt0 / 9;
   const int gend = kt0 < kts1 ? ((min(kt1, kts1) + 8) / 9) * NP : 0;
   int gw = cb0 * NP + wave, cbw = cb0, qw = wave, sw = gw % RP;   // this wave's next piece (NW <= NP)
+  const __amdgpu_buffer_rsrc_t rgs = ph_rsrc(VIRT ? g0.gscale : nullptr, VIRT ? (long long)p.batch * g0.cin * 4 : 0);
+  const __amdgpu_buffer_rsrc_t rgt = ph_rsrc(VIRT ? g0.gshift : nullptr, VIRT ? (long long)p.batch * g0.cin * 4 : 0);
   auto issue_halo = [&](int hi) __attribute__((always_inline)) {
     int n = 0;
     while (gw < hi) {
@@ -1532,7 +1555,20 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_halo_kernel(Params p)
       const unsigned ld2 = (unsigned)(second ? g0.ld1 : g0.ld0) * 2u;
       const int cc = c - (second ? g0.c_split : 0);
       const int rchh = (lane & 7) ^ ((4 * qw + (lrow >> 1)) & 7);
-      const unsigned voff = (unsigned)(hstart + 8 * qw + lrow) * ld2 + (unsigned)(cc + rchh * 8) * 2u;
+      unsigned voff;
+      if constexpr (VIRT) {
+        voff = virt_src(8 * qw + lrow, ld2, (unsigned)(cc + rchh * 8) * 2u);
+        if (qw == 0) {   // the block's GroupNorm scale / shift ride with its first piece
+          float* gb = gnb + (cbw % 3) * 128;
+          const unsigned go = (unsigned)(b0 * g0.cin + c + lane) * 4u;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rgs, (__attribute__((address_space(3))) void*)gb, 4, go, 0, 0, 0);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rgt, (__attribute__((address_space(3))) void*)(gb + 64), 4, go, 0,
+                                                   0, 0);
+          n += 2;
+        }
+      } else {
+        voff = (unsigned)(hstart + 8 * qw + lrow) * ld2 + (unsigned)(cc + rchh * 8) * 2u;
+      }
       ph_dma(second ? d.a1 : d.a0, halo + sw * 512, voff, 0);
       ++n;
       gw += CF::NW;
@@ -1553,10 +1589,54 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_halo_kernel(Params p)
   const int brow16 = wn * CF::TN + r16;
   const int arow16 = wm * CF::TM + r16;
 
-  // prologue: W of the first K-step, the first block's early halo pieces (or the first shortcut tile)
+  // VIRT: GroupNorm (+ SiLU) of n landed pieces starting at this wave's piece (g, cb, q, slot) — lane =
+  // (pixel l >> 3, logical 16-B chunk l & 7), read-modify-write in place; the border pixels become 0
+  auto transform = [&](int n, int tcb, int tq, int tsl) __attribute__((always_inline)) {
+    const int pp = lane >> 3, jc = lane & 7;
+    for (int i = 0; i < n; ++i) {
+      const int h = 8 * tq + pp;
+      const int hr = (int)(((unsigned)h * (unsigned)p.h_divm) >> 20);
+      const int hc = h - hr * HS;
+      const int r = oy0 + hr - 1, c = hc - 1;
+      const bool in = (unsigned)r < (unsigned)g0.h && (unsigned)c < (unsigned)g0.w;
+      half_t* a = halo + tsl * 512 + pp * 64 + ((jc ^ ((h >> 1) & 7)) << 3);
+      const float* gb = gnb + (tcb % 3) * 128 + jc * 8;
+      const h8 v = *reinterpret_cast<const h8*>(a);
+      const f4 sa = *reinterpret_cast<const f4*>(gb), sb = *reinterpret_cast<const f4*>(gb + 4);
+      const f4 ta = *reinterpret_cast<const f4*>(gb + 64), tb = *reinterpret_cast<const f4*>(gb + 68);
+      const float sc[8] = {sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3]};
+      const float sh[8] = {ta[0], ta[1], ta[2], ta[3], tb[0], tb[1], tb[2], tb[3]};
+      h8 o = {};
+      if (in) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float x = (float)v[k] * sc[k] + sh[k];
+          if (g0.silu) x = x * __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+          o[k] = (half_t)x;
+        }
+      }
+      *reinterpret_cast<h8*>(a) = o;
+      tq += CF::NW;
+      if (tq >= NP) { tq -= NP; ++tcb; }
+      tsl += CF::NW;
+      if (tsl >= RP) tsl -= RP;
+    }
+  };
+  // prologue: W of the first K-step, the first block's early halo pieces (or the first shortcut tile);
+  // VIRT: those pieces are transformed before the loop (every wave waits for its own, then a barrier)
   issue_w(kt0, 0);
-  if (kt0 < kts1) issue_halo(min(gend, cb0 * NP + p.h_phi[0]));
-  else issue_a1(kt0, (kt0 - kts1) & 1);
+  if (kt0 < kts1) {
+    const int pg = gw, pcb = cbw, pq = qw, psl = sw;
+    issue_halo(min(gend, cb0 * NP + p.h_phi[0]));
+    if constexpr (VIRT) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      transform((gw - pg) / CF::NW, pcb, pq, psl);
+    }
+  } else {
+    issue_a1(kt0, (kt0 - kts1) & 1);
+  }
+  int xn = 0, xcb = 0, xq = 0, xsl = 0;   // VIRT: this wave's pieces issued last K-step, transformed this one
   int cb = cb0, j = 0;
   int cbslot = (cb0 * NP) % RP;   // slot of the current block's piece 0
 #if !defined(SDK_NO_PRIO)
@@ -1573,11 +1653,20 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_halo_kernel(Params p)
       n = wcnt;
       if (s1) n += issue_a1(kt + 1, (kt + 1 - kts1) & 1);
     }
+    const int ig = gw, icb = cbw, iq = qw, isl = sw;
     if (!s1) n += issue_halo(min(gend, cb * NP + p.h_phi[j + 1]));
     vmcnt_wait_dyn(__builtin_amdgcn_readfirstlane(n));
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (VIRT) {
+      // last K-step's pieces have landed (the wait above); no K-step reads them before the next one
+      transform(xn, xcb, xq, xsl);
+      xn = (gw - ig) / CF::NW;      // pieces (the DMA count also holds a block's scale / shift)
+      xcb = icb;
+      xq = iq;
+      xsl = isl;
+    }
     const half_t* st = lds + ((kt - kt0) & 1) * CF::WSTAGE_H;
     const half_t* ab[CF::FM16];
     int sx[CF::FM16];
@@ -2451,9 +2540,17 @@ int launch_halo(const Params& p, hipStream_t s) {
   if (p.h_rp <= 0 || p.h_rp > CF::MAX_RP || p.h_np > p.h_rp || p.kt_per_split % 9 || kts1 % 9 ||
       (p.nseg > 1 && p.h_rp * 1024 < 2 * CF::TBM * BK * 2))
     return fail(SDK_EINVAL, "conv2d: halo plan out of range");
-  const int lds_bytes = CF::WRING_BYTES + p.h_rp * 1024 + CF::VEC_BYTES;
-  if (int e = ensure_dyn_lds((const void*)conv_halo_kernel<CF>, 160 * 1024, attr_set, "conv2d")) return e;
-  hipLaunchKernelGGL((conv_halo_kernel<CF>), dim3(p.tiles_m * p.tiles_n, p.split), dim3(CF::NT), lds_bytes, s, p);
+  const int lds_bytes = CF::WRING_BYTES + p.h_rp * 1024 + CF::VEC_BYTES + (p.h_virt ? CF::GNB_BYTES : 0);
+  if (p.h_virt) {
+    static std::atomic<unsigned long long> attr_v{0};
+    if (int e = ensure_dyn_lds((const void*)conv_halo_kernel<CF, true>, 160 * 1024, attr_v, "conv2d")) return e;
+    hipLaunchKernelGGL((conv_halo_kernel<CF, true>), dim3(p.tiles_m * p.tiles_n, p.split), dim3(CF::NT), lds_bytes, s,
+                       p);
+  } else {
+    if (int e = ensure_dyn_lds((const void*)conv_halo_kernel<CF, false>, 160 * 1024, attr_set, "conv2d")) return e;
+    hipLaunchKernelGGL((conv_halo_kernel<CF, false>), dim3(p.tiles_m * p.tiles_n, p.split), dim3(CF::NT), lds_bytes,
+                       s, p);
+  }
   return check_launch("conv_halo");
 }
 
@@ -2531,9 +2628,15 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   p.res = (const half_t*)a->residual; p.res_ld = a->res_ld;
   p.out = a->out; p.out_ld = a->out_ld; p.out_mode = a->out_mode;
   bool transform = false;
+  bool transform_other = false;   // any reason but segment 0's own GroupNorm / SiLU prologue
   for (int s = 0; s < a->nseg; ++s) {
     const sdk_conv_src& g = a->seg[s];
     transform |= (g.gn_scale != nullptr) || g.silu;
+    if (s == 1) transform_other |= (g.gn_scale != nullptr) || g.silu;
+    if ((double)a->batch * g.h * g.w * std::max(g.ld0, g.ld1) * 2 >= 2147483647.0) transform_other = true;
+    if (g.c_split < g.cin && g.c_split % BK) transform_other = true;
+    if (s == 1 && (g.ksize != 1 || g.stride != 1 || g.pad != 0 || g.pad_end || g.upsample || g.h != a->ho || g.w != a->wo))
+      transform_other = true;
     // the LDS-DMA kernels: buffer resources (31-bit byte offsets), a K-step's 64 channels
     // from one concat source, and a second segment that is a plain 1x1 over the output grid
     if ((double)a->batch * g.h * g.w * std::max(g.ld0, g.ld1) * 2 >= 2147483647.0) transform = true;
@@ -2541,8 +2644,8 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
     if (s == 1 && (g.ksize != 1 || g.stride != 1 || g.pad != 0 || g.pad_end || g.upsample || g.h != a->ho || g.w != a->wo))
       transform = true;
   }
-  if ((double)((a->cout + 127) / 128 * 128) * a->k_total * 2 >= 2147483647.0) transform = true;
-  if (a->act != SDK_ACT_NONE) transform = true;   // the CLIP fc1 (once per prompt, not per step)
+  if ((double)((a->cout + 127) / 128 * 128) * a->k_total * 2 >= 2147483647.0) transform = transform_other = true;
+  if (a->act != SDK_ACT_NONE) transform = transform_other = true;   // the CLIP fc1 (once per prompt, not per step)
   // tile configuration: LDS-DMA kernels for transform-free operands, scored by
   // padded-work efficiency x whole-chip wave quantisation x measured per-config
   // throughput
@@ -2641,21 +2744,40 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   // variants 36 / 37: halo-tile 3x3 (256x320 / 128x320 tiles) for a pad-0 3x3 conv over a zero-bordered
   // image (nomask, one segment); a plan exists when the tile's padded rows fit the LDS ring on time
   // (halo_sched.h).  Forced but not applicable: the planner's choice, as for the other variants.
-  if (forced == 36 || forced == 37) {
+  // returns 1 when the halo variant v (36 / 37) has a plan for this conv (p / info filled), 0 if not,
+  // or < 0 with an error code
+  auto try_halo = [&](int v) -> int {
     const sdk_conv_src& g = a->seg[0];
     // a second segment is the fused 1x1 shortcut over the output grid (transform excludes other shapes),
     // read in whole 64-channel blocks
     const sdk_conv_src& g1 = a->seg[1];
     const bool seg1_ok = a->nseg == 1 || (g1.cin % BK == 0 && (g1.c_split == g1.cin || g1.c_split % BK == 0));
-    const bool shape_ok = !transform && seg1_ok && g.ksize == 3 && g.stride == 1 && g.pad == 0 &&
-                          g.pad_end == 0 && !g.upsample && p.nomask && a->out_mode != SDK_OUT_GEGLU_F16;
-    const int tbm = forced == 36 ? HCfg256x320::TBM : HCfg128x320::TBM;
+    const int tbm = v == 36 ? HCfg256x320::TBM : HCfg128x320::TBM;
     const int tbn = HCfg256x320::TBN;
-    const int nw = forced == 36 ? HCfg256x320::NW : HCfg128x320::NW;
-    const int max_rp = forced == 36 ? HCfg256x320::MAX_RP : HCfg128x320::MAX_RP;
+    const int nw = v == 36 ? HCfg256x320::NW : HCfg128x320::NW;
+    const int max_rp = v == 36 ? HCfg256x320::MAX_RP : HCfg128x320::MAX_RP;
+    const bool common = seg1_ok && g.ksize == 3 && g.stride == 1 && g.pad_end == 0 && !g.upsample &&
+                        a->out_mode != SDK_OUT_GEGLU_F16;
+    // physical: a pad-0 conv over a zero-bordered input; virtual (GroupNorm-fused): a pad-1 conv over the
+    // raw input with its GroupNorm scale / shift (+ SiLU), whole 64-channel blocks, single-image tiles
+    const bool phys_ok = common && !transform && g.pad == 0 && p.nomask;
+    const bool virt_ok = common && !transform_other && g.gn_scale != nullptr && g.pad == 1 && g.cin % BK == 0 &&
+                         (g.c_split == g.cin || g.c_split % BK == 0) && p.hw_out % tbm == 0;
     HaloPlan hp;
-    if (shape_ok && halo_plan(p.hw_out, p.ho, p.wo, g.h, g.w, tbm, max_rp, nw, &hp) == 0) {
-      p.variant = forced;
+    int divm = 0;
+    bool ok = false;
+    if (phys_ok) {
+      ok = halo_plan(p.hw_out, p.ho, p.wo, g.h, g.w, tbm, max_rp, nw, &hp) == 0;
+    } else if (virt_ok) {
+      ok = halo_plan(p.hw_out, p.ho, p.wo, p.ho + 2, p.wo + 2, tbm, max_rp, nw, &hp, 2) == 0;
+      divm = ok ? ((1 << 20) + hp.hs - 1) / hp.hs : 0;
+      for (int h = 0; ok && h < hp.rh * hp.hs; ++h)      // the kernel's row of a halo pixel: exact here
+        ok = (int)(((unsigned)h * (unsigned)divm) >> 20) == h / hp.hs;
+    }
+    if (ok) {
+      p.variant = v;
+      p.h_virt = virt_ok && !phys_ok;
+      p.h_divm = divm;
       p.tiles_m = (p.M + tbm - 1) / tbm;
       p.tiles_n = (p.N + tbn - 1) / tbn;
       p.Npad = p.tiles_n * tbn;
@@ -2684,7 +2806,7 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
         info->split_k = split;
         info->grid_tiles = tiles;
         info->workspace_bytes = ws;
-        info->variant = forced;
+        info->variant = v;
         info->flops = 2.0 * p.M * (double)p.N * kreal;
         info->gn_chunks = gn_nch;
       }
@@ -2695,7 +2817,19 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
         p.gnp = reinterpret_cast<float2*>(a->gn_partial);
         p.gn_nch = gn_nch;
       }
-      return SDK_OK;
+      return 1;
+    }
+    return 0;
+  };
+  if (forced == 36 || forced == 37) {
+    const int r = try_halo(forced);
+    if (r) return r > 0 ? SDK_OK : r;
+  } else if (forced < 0 && transform && !transform_other) {
+    // a GroupNorm (+ SiLU) prologue on a 3x3: the halo kernel applies it to its staged input (else the
+    // register-staged kernel below)
+    for (int v : {36, 37}) {
+      const int r = try_halo(v);
+      if (r) return r > 0 ? SDK_OK : r;
     }
   }
   // ids: 0 register-staged; 2..7 LDS-DMA configs; 8, 9 phased 256x256; 10..15 diagnostics;

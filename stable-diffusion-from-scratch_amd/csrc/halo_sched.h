@@ -16,8 +16,8 @@
 // The issue schedule tau(q) (K-step relative to the piece's own block start, negative = during
 // the previous block) is greedy-earliest subject to: the slot's previous occupant is dead,
 // tau is monotone in q, at most `cap` pieces per K-step (a block's tau and its successor's tau - 9
-// are the same K-step), and tau(q) <= need(q) - 1 (the K-step
-// that reads a piece waits for DMAs issued at least one K-step before it).  The kernel issues,
+// are the same K-step), and tau(q) <= need(q) - lead (the K-step that reads a piece waits for DMAs
+// issued at least one K-step before it; the GroupNorm-fused form needs one more for the transform).  The kernel issues,
 // at K-step j of block cb, the global pieces [cb*np + phi[j], cb*np + phi[j+1]).
 //
 // Header-only, no HIP: tests/test_halo_schedule.py compiles it with g++ and replays the ring.
@@ -39,7 +39,10 @@ struct HaloPlan {
 // Rows of output pixels a tile of `tbm` consecutive pixels spans, and the halo geometry.
 // src_h / src_w: the padded source (ho + 2, wo + 2).  Returns 0 when the plan exists.
 //   multi-image tiles: tbm % hw == 0 (whole images per tile); single-image: hw % tbm == 0.
-inline int halo_plan(int hw, int ho, int wo, int src_h, int src_w, int tbm, int max_rp, int cap, HaloPlan* out) {
+// lead: K-steps between a piece's issue and its first read (1: read as landed; 2: the GroupNorm-fused
+// form transforms a piece in LDS the K-step after it lands, before it is read)
+inline int halo_plan(int hw, int ho, int wo, int src_h, int src_w, int tbm, int max_rp, int cap, HaloPlan* out,
+                     int lead = 1) {
   if (src_h != ho + 2 || src_w != wo + 2 || hw != ho * wo || tbm <= 0 || cap <= 0) return 1;
   const bool multi = tbm % hw == 0;
   if (!multi && hw % tbm) return 2;
@@ -89,7 +92,7 @@ inline int halo_plan(int hw, int ho, int wo, int src_h, int src_w, int tbm, int 
     int lo = q >= ep ? dead[q - ep] - 8 : -9;     // the occupant (cb-1, q-ep) died at K-step dead - 9
     lo = std::max(std::max(lo, prev), -9);
     while (lo <= 8 && cnt[(lo + 9) % 9] >= cap) ++lo;
-    if (lo > 8 || lo > need[q] - 1) return 4;     // not in time: the ring is too small for this tile
+    if (lo > 8 || lo > need[q] - lead) return 4;  // not in time: the ring is too small for this tile
     tau[q] = lo;
     ++cnt[(lo + 9) % 9];
     prev = lo;

@@ -855,6 +855,24 @@ static const int g_gn_part_fused_max_hw = [] {
   return e ? atoi(e) : 256;
 }();
 
+extern "C" int sdk_group_norm_finalize(const sdk_group_norm_args* a, const float* part0, int32_t nch0,
+                                       const float* part1, int32_t nch1, sdk_stream_t stream) {
+  if (!a || !a->src0 || !a->scale || !a->shift) return fail(SDK_EINVAL, "group_norm_finalize: null pointer");
+  if (a->channels % 8 || a->groups <= 0 || a->channels % a->groups || a->c_split % 8 || a->c_split <= 0 ||
+      a->c_split > a->channels)
+    return fail(SDK_EINVAL, "group_norm_finalize: channels/c_split must be multiples of 8, channels % groups == 0");
+  const bool concat = a->c_split < a->channels;
+  const bool parts = part0 && (!concat || part1);
+  if (!parts) return sdk_group_norm_affine(a, stream);
+  if (nch0 <= 0 || a->hw % nch0 || (concat && (nch1 <= 0 || a->hw % nch1)))
+    return fail(SDK_EINVAL, "group_norm_finalize: partial chunks must divide hw");
+  if (a->batch <= 0) return SDK_OK;
+  hipLaunchKernelGGL(gn_finalize_part_kernel, dim3(a->groups, a->batch), dim3(256), 0, (hipStream_t)stream,
+                     (const float2*)part0, nch0, (const float2*)part1, nch1, a->c_split, a->hw, a->channels, a->groups,
+                     a->eps, a->gamma, a->beta, a->scale, a->shift);
+  return check_launch("gn_finalize_part");
+}
+
 extern "C" int sdk_group_norm(const sdk_group_norm_args* a, int32_t silu, void* y, int32_t ld_y, int32_t h, int32_t w,
                               int32_t pad, const float* part0, int32_t nch0, const float* part1, int32_t nch1,
                               sdk_stream_t stream) {

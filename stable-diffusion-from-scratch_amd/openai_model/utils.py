@@ -24,6 +24,11 @@ class GroupNorm32(nn.GroupNorm):
     def stats(self, x):
         return ops.group_norm_affine(x, self._g, self._b, self.eps, self.num_groups)
 
+    def scale_shift(self, x):
+        """(scale, shift) [B, C] of this GroupNorm of x (from the producers' statistics) for a conv that
+        applies it to its own staged input (ops.group_norm_scale_shift)."""
+        return ops.group_norm_scale_shift(x, self._g, self._b, self.eps, self.num_groups)
+
     def norm(self, x, silu=True, pad=0):
         """GroupNorm (+ SiLU) of x materialised (zero-bordered by ``pad``) — one ``sdk_group_norm``."""
         return ops.group_norm(x, self._g, self._b, self.eps, self.num_groups, silu=silu, pad=pad)

@@ -249,20 +249,25 @@ class _Autotune:
         hit = self.table.get(key)
         if hit is not None or not self.enabled or torch.cuda.is_current_stream_capturing():
             return hit
-        if a.seg[0].gn_scale or a.seg[0].silu or (a.nseg > 1 and (a.seg[1].gn_scale or a.seg[1].silu)):
+        cands = self.VARIANTS
+        if a.nseg > 1 and (a.seg[1].gn_scale or a.seg[1].silu):
             self.table[key] = (0, 0)
             return self.table[key]
+        if a.seg[0].gn_scale or a.seg[0].silu:
+            # a transform prologue: the register-staged kernel, or the halo-tile 3x3 with GroupNorm (+ SiLU)
+            # applied to its staged input (variants 36 / 37, when a plan exists)
+            cands = (0, 36, 37)
         best, best_t = (0, 0), float("inf")
         info = ConvPlanInfo()
         stream = _stream()
         emit_any = False
         if gn:                           # is there a candidate at all that emits the statistics?
-            for v in self.VARIANTS:
+            for v in cands:
                 for sp in self.SPLITS:
                     a.variant_hint, a.split_k = v + 1, sp
                     if lib().sdk_conv2d_plan(C.byref(a), C.byref(info)) == 0 and info.gn_chunks > 0:
                         emit_any = True
-        for v in self.VARIANTS:
+        for v in cands:
             for sp in self.SPLITS:
                 a.variant_hint, a.split_k = v + 1, sp
                 if lib().sdk_conv2d_plan(C.byref(a), C.byref(info)) != 0:
@@ -576,6 +581,74 @@ def gelu(x):
 def group_norm_silu(x, gamma, beta, eps, groups=32):
     """GroupNorm + SiLU materialised once (stats pass + apply pass) — the input of a 3x3 conv."""
     return group_norm_apply(x, group_norm_affine(x, gamma, beta, eps, groups), silu=True)
+
+
+def group_norm_scale_shift(x, gamma, beta, eps, groups=32):
+    """Per-(batch, channel) fp32 (scale, shift) [B, C] of GroupNorm(x) from the statistics its producing
+    convs emitted (else a statistics pass) — for a 3x3 conv that applies GroupNorm + SiLU to its own
+    staged input (``conv2d(gn=(scale, shift), silu=True, pad=1)`` on the halo-tile kernel), so the
+    normalised tensor is never written (``sdk_group_norm_finalize``)."""
+    args, (B, H, W, Ch), dev = _gn_args(x)
+    args.groups, args.eps = groups, eps
+    args.gamma, args.beta = gamma.data_ptr(), beta.data_ptr()
+    scale = torch.empty(B, Ch, dtype=torch.float32, device=dev)
+    shift = torch.empty(B, Ch, dtype=torch.float32, device=dev)
+    args.scale, args.shift = scale.data_ptr(), shift.data_ptr()
+    ws = WORKSPACE.get(lib().sdk_group_norm_workspace(B, H * W, Ch), dev)
+    args.workspace, args.workspace_bytes = ws.data_ptr(), ws.numel()
+    srcs = [t for t in _as_pair(x) if t is not None]
+    parts = [getattr(t, GN_ATTR, None) for t in srcs]
+    parts = [pp if pp is not None and pp[2] == t._version else None for pp, t in zip(parts, srcs)]
+    p0 = p1 = None
+    n0 = n1 = 0
+    if all(pp is not None for pp in parts):
+        (p0, n0, _) = parts[0]
+        if len(parts) > 1:
+            (p1, n1, _) = parts[1]
+    if PROFILER.active:
+        PROFILER.begin("group_norm", None)
+    check(lib().sdk_group_norm_finalize(C.byref(args), _ptr(p0), n0, _ptr(p1), n1, _stream()), "group_norm_finalize")
+    if PROFILER.active:
+        PROFILER.end()
+    return scale, shift
+
+
+# ResBlock 3x3 convs apply GroupNorm + SiLU to their own staged input (no normalised tensor written) where
+# the halo-tile kernel has a plan; SD_AMD_FUSED_GN_CONV=0 keeps the materialised zero-bordered GN output
+FUSED_GN_CONV = __import__("os").environ.get("SD_AMD_FUSED_GN_CONV", "0") == "1"
+_FUSABLE = {}
+
+
+def gn_conv_fusable(pc: "PackedConv", B, H, W, c0, c1=0) -> bool:
+    """Does the halo-tile kernel take ``conv2d(pc, x, gn=..., silu=True, pad=1)`` (3x3, GroupNorm-fused) for
+    an NHWC input [B, H, W, c0] (+ a concatenated [.., c1])?  A host-side plan query (no launch), cached."""
+    if not FUSED_GN_CONV or pc.seg_geom[0][0] != 3:
+        return False
+    key = (B, H, W, c0, c1, pc.N, pc.k_total, len(pc.seg_geom))
+    hit = _FUSABLE.get(key)
+    if hit is not None:
+        return hit
+    Cin = c0 + c1
+    ok = False
+    for v in (36, 37):
+        a = ConvArgs()
+        s = a.seg[0]
+        s.src0 = 0x1000
+        s.src1 = 0x2000 if c1 else None
+        s.c_split, s.cin, s.ld0, s.ld1 = c0, Cin, c0, c1
+        s.h, s.w, s.ksize, s.stride, s.pad = H, W, 3, 1, 1
+        s.gn_scale, s.gn_shift, s.silu = 0x3000, 0x4000, 1
+        a.nseg = 1
+        a.batch, a.ho, a.wo, a.cout = B, H, W, pc.N
+        a.weight, a.out, a.out_ld, a.out_mode = 0x5000, 0x6000, pc.N, OUT_NHWC_F16
+        a.k_total = pc.seg_geom[0][1] // BK * BK * 9 if pc.seg_geom[0][1] % BK == 0 else -1
+        a.variant_hint = v + 1
+        info = ConvPlanInfo()
+        if a.k_total > 0 and lib().sdk_conv2d_plan(C.byref(a), C.byref(info)) == 0 and info.variant == v:
+            ok = True
+            break
+    _FUSABLE[key] = ok
+    return ok
 
 
 def group_norm_affine(x, gamma, beta, eps, groups=32):

@@ -2,7 +2,9 @@
 // the per-wave issue state machine of the kernel, then every A-fragment read of every K-step of every
 // tile is checked to find (a) its own block's piece in the slot, (b) a piece issued at least one K-step
 // earlier (the counted vmcnt wait covers only those), (c) the padded input pixel the tap addresses.
-// usage: halo_sim batch ho wo tbm nw max_rp ncb split  -> prints "OK np rp phi..." or "FAIL ..."
+// usage: halo_sim batch ho wo tbm nw max_rp ncb split [lead]  -> prints "OK np rp phi..." or "FAIL ..."
+// lead 2 (the GroupNorm-fused form): a piece is also transformed in LDS at the K-step after its issue, so
+// it must be issued at least two K-steps before its first read.
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -12,12 +14,13 @@
 using namespace sdk;
 
 int main(int argc, char** argv) {
-  if (argc != 9) return 2;
+  if (argc != 9 && argc != 10) return 2;
+  const int lead = argc == 10 ? atoi(argv[9]) : 1;
   const int batch = atoi(argv[1]), ho = atoi(argv[2]), wo = atoi(argv[3]), tbm = atoi(argv[4]);
   const int nw = atoi(argv[5]), max_rp = atoi(argv[6]), ncb = atoi(argv[7]), split_req = atoi(argv[8]);
   const int hw = ho * wo, M = batch * hw, sh = ho + 2, sw_ = wo + 2;
   HaloPlan hp;
-  const int rc = halo_plan(hw, ho, wo, sh, sw_, tbm, max_rp, nw, &hp);
+  const int rc = halo_plan(hw, ho, wo, sh, sw_, tbm, max_rp, nw, &hp, lead);
   if (rc) {
     printf("NOPLAN %d\n", rc);
     return 0;
@@ -57,7 +60,7 @@ int main(int argc, char** argv) {
           }
         }
       };
-      issue(std::min(gend, cb0 * NP + hp.phi[0]), kt0 - 1);
+      issue(std::min(gend, cb0 * NP + hp.phi[0]), kt0 - 10);   // prologue: waited (and transformed) before the loop
       int cb = cb0, j = 0, cbslot = (cb0 * NP) % RP;
       for (int kt = kt0; kt < kt1; ++kt) {
         issue(std::min(gend, cb * NP + hp.phi[j + 1]), kt);
@@ -75,7 +78,7 @@ int main(int argc, char** argv) {
             printf("FAIL tile %d kt %d pix %d: slot %d holds %lld, want %lld\n", tm, kt, pix, slot, ring[slot], want);
             return 1;
           }
-          if (issued_at[want] >= kt) {
+          if (issued_at[want] > kt - lead) {
             printf("FAIL tile %d kt %d: piece %lld issued at %d (not before the read)\n", tm, kt, want,
                    issued_at[want]);
             return 1;

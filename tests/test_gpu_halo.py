@@ -141,3 +141,74 @@ def test_halo_fused_shortcut_segment(ops, variant, B, H, W, C0, C1, C2, Co, spli
     if split == 1:
         yt = ops.conv2d(pc, hp, pad=0, seg2=(res_src, None, False), variant=TWIN[variant], split_k=1)
         assert torch.equal(y, yt)
+
+
+@pytest.mark.parametrize("variant", [36, 37])
+@pytest.mark.parametrize("B,H,W,C0,C1,Co,split,skip", [
+    (2, 64, 64, 320, 0, 320, 1, None),          # ResBlock conv1 at the 64x64 level
+    (2, 32, 32, 320, 320, 640, 1, None),        # decoder conv1 over a 2-source concat
+    (2, 32, 32, 640, 0, 640, 1, "residual"),    # conv2 + identity skip
+    (2, 32, 32, 640, 0, 640, 1, "fused"),       # conv2 + nin_shortcut as a second K segment
+    (1, 16, 16, 1280, 0, 1280, 4, None),        # 16x16 level, split-K on channel blocks
+    (1, 48, 48, 320, 0, 320, 1, None),          # tiles not row-aligned (C5-shaped level)
+])
+def test_halo_groupnorm_fused_equals_materialised(ops, variant, B, H, W, C0, C1, Co, split, skip):
+    """GroupNorm + SiLU applied by the halo kernel to its own staged input (raw input, pad 1, virtual zero
+    border) equals the conv over the materialised zero-bordered GN output (sdk_group_norm_apply_padded,
+    pad 0) BIT FOR BIT — the same transform arithmetic, the same K order — with the embedding row, the
+    residual / fused shortcut and the emitted statistics; and matches an fp32 reference."""
+    g = torch.Generator().manual_seed(B * 131 + H + C0 + C1)
+    a = (torch.randn(B, H, W, C0, generator=g) * 2 + 0.5).half()
+    c = (torch.randn(B, H, W, C1, generator=g) - 1).half() if C1 else None
+    src = (a.to(DEV), c.to(DEV)) if C1 else a.to(DEV)
+    Ci = C0 + C1
+    gamma = (torch.rand(Ci, generator=g) + 0.5).to(DEV)
+    beta = (torch.randn(Ci, generator=g) * 0.2).to(DEV)
+    sc, sh = ops.group_norm_affine(src, gamma, beta, 1e-5, 32)
+    w = torch.randn(Co, Ci, 3, 3, generator=g) / math.sqrt(Ci * 9)
+    b = torch.randn(Co, generator=g) * 0.1
+    emb = torch.randn(B, Co, generator=g)
+    segs, kw = [(w, Ci)], dict(row_bias=(emb.to(DEV), 0), gn_stats=True, split_k=split)
+    xin = torch.cat([a, c], -1) if C1 else a
+    if skip == "residual":
+        res = _rand(B, H, W, Co, seed=3)
+        kw["residual"] = res.to(DEV)
+    elif skip == "fused":
+        s_in = _rand(B, H, W, 192, seed=4)
+        ws = torch.randn(Co, 192, 1, 1, generator=g) / math.sqrt(192)
+        segs.append((ws, 192))
+        kw["seg2"] = (s_in.to(DEV), None, False)
+    pc = ops.PackedConv(segs, b, device=DEV)
+    y, ran = _ran(ops, lambda: ops.conv2d(pc, src, pad=1, gn=(sc, sh), silu=True, variant=variant, **kw))
+    assert ran == variant, "the GroupNorm-fused halo plan should exist for this shape"
+    xa = ops.group_norm_apply(src, (sc, sh), silu=True, pad=1)
+    ym, ranm = _ran(ops, lambda: ops.conv2d(pc, xa, pad=0, variant=variant, **kw))
+    assert ranm == variant
+    assert torch.equal(y, ym), "fused GroupNorm differs from the materialised one"
+    pp, nch, _ = getattr(y, ops.GN_ATTR)
+    pm, nchm, _ = getattr(ym, ops.GN_ATTR)
+    assert nch == nchm and torch.equal(pp, pm)
+    # fp32 reference of the whole block
+    xr = xin.float().permute(0, 3, 1, 2)
+    xn = F.silu(F.group_norm(xr, 32, gamma.cpu(), beta.cpu(), 1e-5)).half().float()
+    ref = F.conv2d(xn, w.half().float(), b, padding=1).permute(0, 2, 3, 1) + emb[:, None, None, :]
+    if skip == "residual":
+        ref = ref + res.float()
+    elif skip == "fused":
+        ref = ref + F.conv2d(s_in.float().permute(0, 3, 1, 2), ws.half().float()).permute(0, 2, 3, 1)
+    assert rel_l2(y, ref) < 3e-3
+
+
+def test_groupnorm_finalize_from_producer_statistics(ops):
+    """sdk_group_norm_finalize from the statistics a producing conv emitted equals the statistics pass."""
+    g = torch.Generator().manual_seed(77)
+    x = _rand(2, 32, 32, 128, seed=8)
+    w = torch.randn(320, 128, 3, 3, generator=g) / math.sqrt(128 * 9)
+    pc = ops.PackedConv([(w, 128)], torch.randn(320, generator=g) + 1, device=DEV)
+    y = ops.conv2d(pc, _padded(x).to(DEV), pad=0, gn_stats=True, variant=36)
+    assert getattr(y, ops.GN_ATTR, None) is not None
+    gamma = (torch.rand(320, generator=g) + 0.5).to(DEV)
+    beta = (torch.randn(320, generator=g) * 0.1).to(DEV)
+    s1, t1 = ops.group_norm_scale_shift(y, gamma, beta, 1e-5, 32)
+    s0, t0 = ops.group_norm_affine(y.clone(), gamma, beta, 1e-5, 32)
+    assert rel_l2(s1, s0) < 1e-5 and rel_l2(t1, t0) < 1e-5
