@@ -37,12 +37,20 @@ CASES = [
     (3, 8, 8, 256, 16, 77, 4, 1, False),       # 4 images per tile overflow the ring
     (16, 128, 128, 256, 16, 77, 8, 1, True),   # VAE 128x128 (one row-half per tile)
     (2, 16, 16, 128, 8, 20, 3, 1, False),      # ring smaller than the live pieces
+    # GroupNorm-fused form (lead 2: transformed in LDS the K-step after landing), 76-slot ring
+    (16, 64, 64, 256, 16, 76, 5, 1, True, 2),
+    (16, 32, 32, 256, 16, 76, 10, 2, True, 2),
+    (16, 16, 16, 256, 16, 76, 20, 4, True, 2),
+    (16, 16, 16, 128, 8, 76, 40, 8, True, 2),
+    (8, 96, 96, 128, 8, 76, 5, 1, True, 2),
+    (8, 48, 48, 256, 16, 76, 10, 3, True, 2),
 ]
 
 
 @pytest.mark.parametrize("case", CASES, ids=[",".join(map(str, c[:8])) for c in CASES])
 def test_halo_ring_replay(sim, case):
-    *args, expect = case
+    args, expect, lead = list(case[:8]), case[8], case[9:]
+    args += list(lead)
     out = subprocess.run([sim, *map(str, args)], capture_output=True, text=True)
     assert out.returncode == 0, out.stdout + out.stderr
     line = out.stdout.strip()
