@@ -1545,8 +1545,12 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_halo_kernel(Params p)
   const int cb0 = kt0 / 9;
   const int gend = kt0 < kts1 ? ((min(kt1, kts1) + 8) / 9) * NP : 0;
   int gw = cb0 * NP + wave, cbw = cb0, qw = wave, sw = gw % RP;   // this wave's next piece (NW <= NP)
-  const __amdgpu_buffer_rsrc_t rgs = ph_rsrc(VIRT ? g0.gscale : nullptr, VIRT ? (long long)p.batch * g0.cin * 4 : 0);
-  const __amdgpu_buffer_rsrc_t rgt = ph_rsrc(VIRT ? g0.gshift : nullptr, VIRT ? (long long)p.batch * g0.cin * 4 : 0);
+  // GroupNorm scale / shift: one buffer resource over the byte range from the lower to the higher array
+  const float* glo = VIRT ? (g0.gscale < g0.gshift ? g0.gscale : g0.gshift) : nullptr;
+  const unsigned goff_s = VIRT ? (unsigned)((const char*)g0.gscale - (const char*)glo) : 0u;
+  const unsigned goff_t = VIRT ? (unsigned)((const char*)g0.gshift - (const char*)glo) : 0u;
+  const __amdgpu_buffer_rsrc_t rgs = ph_rsrc(glo, VIRT ? (long long)(goff_s > goff_t ? goff_s : goff_t) +
+                                                          (long long)p.batch * g0.cin * 4 : 0);
   auto issue_halo = [&](int hi) __attribute__((always_inline)) {
     int n = 0;
     while (gw < hi) {
@@ -1561,9 +1565,10 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_halo_kernel(Params p)
         if (qw == 0) {   // the block's GroupNorm scale / shift ride with its first piece
           float* gb = gnb + (cbw % 3) * 128;
           const unsigned go = (unsigned)(b0 * g0.cin + c + lane) * 4u;
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rgs, (__attribute__((address_space(3))) void*)gb, 4, go, 0, 0, 0);
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rgt, (__attribute__((address_space(3))) void*)(gb + 64), 4, go, 0,
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rgs, (__attribute__((address_space(3))) void*)gb, 4, go + goff_s, 0,
                                                    0, 0);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rgs, (__attribute__((address_space(3))) void*)(gb + 64), 4,
+                                                   go + goff_t, 0, 0, 0);
           n += 2;
         }
       } else {
@@ -1601,21 +1606,22 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_halo_kernel(Params p)
       const bool in = (unsigned)r < (unsigned)g0.h && (unsigned)c < (unsigned)g0.w;
       half_t* a = halo + tsl * 512 + pp * 64 + ((jc ^ ((h >> 1) & 7)) << 3);
       const float* gb = gnb + (tcb % 3) * 128 + jc * 8;
-      const h8 v = *reinterpret_cast<const h8*>(a);
-      const f4 sa = *reinterpret_cast<const f4*>(gb), sb = *reinterpret_cast<const f4*>(gb + 4);
-      const f4 ta = *reinterpret_cast<const f4*>(gb + 64), tb = *reinterpret_cast<const f4*>(gb + 68);
-      const float sc[8] = {sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3]};
-      const float sh[8] = {ta[0], ta[1], ta[2], ta[3], tb[0], tb[1], tb[2], tb[3]};
-      h8 o = {};
-      if (in) {
+      // two 4-channel halves (register budget: the 16-wave tile runs at the 128-VGPR cap)
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          float x = (float)v[k] * sc[k] + sh[k];
-          if (g0.silu) x = x * __builtin_amdgcn_rcpf(1.0f + __expf(-x));
-          o[k] = (half_t)x;
+      for (int hf = 0; hf < 2; ++hf) {
+        const h4 v = *reinterpret_cast<const h4*>(a + 4 * hf);
+        const f4 sc = *reinterpret_cast<const f4*>(gb + 4 * hf), sh = *reinterpret_cast<const f4*>(gb + 64 + 4 * hf);
+        h4 o = {};
+        if (in) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            float x = (float)v[k] * sc[k] + sh[k];
+            if (g0.silu) x = x * __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+            o[k] = (half_t)x;
+          }
         }
+        *reinterpret_cast<h4*>(a + 4 * hf) = o;
       }
-      *reinterpret_cast<h8*>(a) = o;
       tq += CF::NW;
       if (tq >= NP) { tq -= NP; ++tcb; }
       tsl += CF::NW;
@@ -1659,14 +1665,6 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_halo_kernel(Params p)
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (VIRT) {
-      // last K-step's pieces have landed (the wait above); no K-step reads them before the next one
-      transform(xn, xcb, xq, xsl);
-      xn = (gw - ig) / CF::NW;      // pieces (the DMA count also holds a block's scale / shift)
-      xcb = icb;
-      xq = iq;
-      xsl = isl;
-    }
     const half_t* st = lds + ((kt - kt0) & 1) * CF::WSTAGE_H;
     const half_t* ab[CF::FM16];
     int sx[CF::FM16];
@@ -1701,6 +1699,16 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_halo_kernel(Params p)
         for (int i = 0; i < CF::FM16; ++i)
           acc16[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb, fa[i], acc16[i][jj], 0, 0, 0);
       }
+    }
+    if constexpr (VIRT) {
+      // last K-step's pieces have landed (this K-step's wait); no K-step reads them before the next one.
+      // Placed after the MFMAs: the VALU work runs under the matrix pipe and the closing barrier's wait
+      __builtin_amdgcn_sched_barrier(0);
+      transform(xn, xcb, xq, xsl);
+      xn = (gw - ig) / CF::NW;      // pieces (the DMA count also holds a block's scale / shift)
+      xcb = icb;
+      xq = iq;
+      xsl = isl;
     }
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();      // everyone done reading this K-step's W stage and A slots

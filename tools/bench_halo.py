@@ -70,7 +70,28 @@ def main():
         best = {}
         for us, v, s in res:
             best.setdefault(v, (us, s))
-        line = "  ".join(f"v{v}/s{s} {u:6.1f}us {flop / u / 1e6:5.0f}TF" for v, (u, s) in sorted(best.items()))
+        if os.environ.get("HALO_GN") == "1" and not sk:
+            # the GroupNorm-fused form (raw input, pad 1, GN + SiLU applied in LDS) vs the GN apply pass that
+            # the physical form needs in front of it
+            xr = torch.randn(B, H, W, Ci, device="cuda").half()
+            sc = torch.rand(B, Ci, device="cuda") + 0.5
+            sh = torch.randn(B, Ci, device="cuda") * 0.1
+            for var in (36, 37):
+                for sp in splits:
+                    f = lambda: ops.conv2d(pc, xr, pad=1, gn=(sc, sh), silu=True, variant=var, split_k=sp)  # noqa
+                    ops.PROFILER.start()
+                    f()
+                    ops.PROFILER.stop()
+                    rec = ops.PROFILER.records[-1]
+                    if rec[1] != var or rec[5][4] != sp:
+                        continue
+                    us = graph_us(f)
+                    key = 100 + var
+                    if key not in best or us < best[key][0]:
+                        best[key] = (us, sp)
+            best[999] = (graph_us(lambda: ops.group_norm_apply(xr, (sc, sh), silu=True, pad=1)), 0)
+        line = "  ".join((f"v{v}/s{s} " if v < 100 else f"gn{v - 100}/s{s} " if v < 999 else "gnapply ") +
+                         f"{u:6.1f}us {flop / u / 1e6:5.0f}TF" for v, (u, s) in sorted(best.items()))
         print(f"{B}x{H}x{W} {Ci}->{Co}{'+' + str(sk[0]) if sk else ''}: {line}", flush=True)
         del xp, w, pc
 
