@@ -12,6 +12,7 @@
 #include "common.h"
 
 namespace sdk {
+typedef unsigned int u4 __attribute__((ext_vector_type(4)));
 namespace {
 
 template <bool M16>
@@ -65,10 +66,76 @@ __global__ void __launch_bounds__(256) copy_probe_kernel(const h8* src, h8* dst,
   for (; i < n; i += stride) dst[i] = src[i];
 }
 
+// LDS-DMA fill rate (diagnostic, tools/probe_dma.py): every wave of a workgroup streams 1-KiB pieces
+// (64 lanes x 16 B, one buffer_load ... lds) from `src` into its own LDS ring, keeping INF pieces in
+// flight (counted vmcnt), `pieces` per wave; consecutive waves / workgroups read consecutive pieces,
+// wrapped at `bytes` (2 MiB: L2-resident and shared by every CU; 1 GiB: HBM).  MODE 1: the same bytes
+// through registers (buffer_load_dwordx4 + ds_write_b128).  The caller divides bytes moved by time.
+template <int NW, int INF, int MODE>
+__global__ void __launch_bounds__(NW * 64) dma_probe_kernel(const half_t* src, long long bytes, int pieces,
+                                                            float* sink) {
+  extern __shared__ __attribute__((aligned(16))) half_t lds[];
+  constexpr int RING = 128 / NW;                       // pieces per wave (128 KiB per workgroup)
+  static_assert(RING > INF, "ring");
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<half_t*>(src), 0,
+                                                                   (int)std::min(bytes, 0x7fffffffLL), 0x00020000);
+  const long long np = bytes / 1024;
+  long long g = ((long long)blockIdx.x * NW + wave) * pieces;
+  half_t* ring = lds + wave * RING * 512;
+  u4 held[INF];
+  if constexpr (MODE == 0) {
+    for (int i = 0; i < pieces; ++i, ++g) {
+      const unsigned off = (unsigned)((g % np) * 1024) + lane * 16u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(ring + (i % RING) * 512), 16,
+                                               off, 0, 0, 0);
+      if (i >= INF) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INF) : "memory");
+    }
+  } else {
+    // rounds of INF loads in flight; each round's data is written to LDS as the next round issues
+    for (int i = 0; i < pieces; i += INF, g += INF) {
+#pragma unroll
+      for (int u = 0; u < INF; ++u) {
+        if (i > 0) *reinterpret_cast<u4*>(ring + ((i - INF + u) % RING) * 512 + lane * 8) = held[u];
+        held[u] = __builtin_amdgcn_raw_buffer_load_b128(r, (unsigned)(((g + u) % np) * 1024) + lane * 16u, 0, 0);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) sink[blockIdx.x] = (float)lds[lane * 8] + (MODE ? (float)held[0][0] : 0.f);
+}
+
 }  // namespace
 }  // namespace sdk
 
 using namespace sdk;
+
+// diagnostics only (not in sdk_amd.h): one launch of the LDS-DMA fill probe, nw in {4, 8, 16} waves per
+// workgroup, inflight in {1, 2, 4, 6} pieces per wave, mode 0 LDS-DMA / 1 register staging
+extern "C" int sdk_probe_dma(int32_t nw, int32_t inflight, int32_t mode, const void* src, int64_t bytes, int32_t pieces,
+                             int32_t blocks, float* sink, sdk_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+#define SDK_DP(NW_, INF_, MODE_)                                                                                   \
+  if (nw == NW_ && inflight == INF_ && mode == MODE_) {                                                            \
+    static bool attr = false;                                                                                       \
+    if (!attr) {                                                                                                    \
+      hipFuncSetAttribute((const void*)dma_probe_kernel<NW_, INF_, MODE_>,                                          \
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);                                 \
+      attr = true;                                                                                                  \
+    }                                                                                                               \
+    hipLaunchKernelGGL((dma_probe_kernel<NW_, INF_, MODE_>), dim3(blocks), dim3(NW_ * 64), 128 * 1024, s,            \
+                       (const half_t*)src, (long long)bytes, pieces, sink);                                         \
+    return check_launch("probe_dma");                                                                               \
+  }
+  SDK_DP(4, 1, 0) SDK_DP(4, 2, 0) SDK_DP(4, 4, 0) SDK_DP(4, 6, 0)
+  SDK_DP(8, 1, 0) SDK_DP(8, 2, 0) SDK_DP(8, 4, 0) SDK_DP(8, 6, 0)
+  SDK_DP(16, 1, 0) SDK_DP(16, 2, 0) SDK_DP(16, 4, 0) SDK_DP(16, 6, 0)
+  SDK_DP(8, 2, 1) SDK_DP(8, 4, 1) SDK_DP(16, 2, 1) SDK_DP(16, 4, 1)
+#undef SDK_DP
+  return fail(SDK_EINVAL, "probe_dma: unsupported (nw, inflight, mode)");
+}
 
 // FLOPs of one launch of the MFMA probe (2*M*N*K per MFMA x MFMAs per wave x waves)
 extern "C" double sdk_probe_mfma_flops(int32_t m16, int32_t blocks, int32_t iters) {
