@@ -102,6 +102,10 @@ typedef struct {
                               gn_chunks > 0): [batch][gn_chunks][cout] float pairs (mean, M2) over
                               ho*wo/gn_chunks output pixels each — sdk_group_norm merges them instead of
                               a statistics pass over the tensor */
+  int64_t weight_batch_stride;  /* 0, or per-image weights: output rows of image b (b = m / (ho*wo)) use
+                                   weight + b * weight_batch_stride (elements); only the LDS-DMA tile
+                                   kernels, with M-tiles inside one image (the reassociated
+                                   cross-attention's per-prompt matrices) */
 } sdk_conv_args;
 
 enum sdk_conv_act {
@@ -249,6 +253,17 @@ typedef struct {
 } sdk_xattn_ln_args;
 
 int sdk_cross_attention_block_ln(const sdk_xattn_args* a, const sdk_xattn_ln_args* ln, sdk_stream_t stream);
+
+/* ---------------------------------------------------------------- segment softmax
+ * p[m, h*seglen + j] = softmax_j(scale * s[m, h*seglen + j]) for each of nseg segments of a row (fp32 in,
+ * fp16 out), columns [nseg*seglen, ld_p) of p written as zeros (the K padding of the GEMM that consumes
+ * p).  The middle step of the reassociated cross-attention at the 1280-channel levels, where the
+ * scores of all heads against the cached context come out of ONE GEMM with per-prompt weights
+ * (K_h Wq_h per head, sdk_conv_args.weight_batch_stride) and the output of another (Wo_h V_h^T).
+ * Replaces: the sim.softmax(dim=-1) of CrossAttention.forward (openai_model/attention.py:106-112, in
+ * flash_attn_func at the call sites :216-257).  seglen <= 128. */
+int sdk_segment_softmax(const float* s, int32_t ld_s, void* p, int32_t ld_p, int32_t rows, int32_t nseg,
+                        int32_t seglen, float scale, sdk_stream_t stream);
 
 /* ---------------------------------------------------------------- sampler / glue
  * DDIM update (DDIM/ddim.py:194-204 == ldm/diffusion/ddim.py:197-205), fp32,

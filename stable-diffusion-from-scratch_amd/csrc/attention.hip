@@ -63,14 +63,17 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long lo
 }
 
 // CAUSAL is a template flag: the SD UNet's non-causal instantiations carry no masking code
-template <int DQK, int DV, int NW, int QB, bool CAUSAL = false>
-__global__ void __launch_bounds__(NW * 64, QB == 2 ? 1 : 2) attn_fwd_kernel(AttnParams p) {
+template <int DQK, int DV, int NW, int QB, bool CAUSAL = false, bool STAG = false, int QSD = 0>
+__global__ void __launch_bounds__(NW * 64, (STAG && DQK <= 64) ? 4 : QB == 2 ? 1 : 2) attn_fwd_kernel(AttnParams p) {
+  static_assert(!STAG || (QB == 1 && NW % 2 == 0), "stagger: one query block per wave, paired waves");
+  static_assert(QSD == 0 || (!CAUSAL && QSD % 8 == 0 && QSD < DQK), "score seed column: a padding column of Q/K");
+  constexpr int NB = STAG ? 3 : 2;   // LDS stages
   constexpr int NT = NW * 64;
   constexpr int KLD = DQK + 8;                                       // K row stride (halfs)
   constexpr int VLD = ((DV * 2 / 64) % 2 == 0) ? DV + 32 : DV;       // V row stride: 64 or 192 B mod 256
   constexpr int KS = KT * KLD, STAGE = KS + KT * VLD;
   constexpr int SL = (KT * (DQK / 8) + NT - 1) / NT;                 // staging slots per thread (K and V each)
-  __shared__ __attribute__((aligned(16))) half_t smem[2 * STAGE];
+  __shared__ __attribute__((aligned(16))) half_t smem[NB * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 31, fh = lane >> 5;
@@ -86,11 +89,11 @@ __global__ void __launch_bounds__(NW * 64, QB == 2 ? 1 : 2) attn_fwd_kernel(Attn
   const int d = p.d, nch = (d + 7) >> 3;   // real 16-B chunks per row
   const bool ones_row = d < DV;            // row sum from the PV MFMA (ones column at d)
 
-  // zero the LDS padding of both stages once (K columns >= 8*nch, V columns >= 8*nch),
+  // zero the LDS padding of every stage once (K columns >= 8*nch, V columns >= 8*nch),
   // with the ones column at d; the staged chunks never touch it
-  for (int e = tid; e < 2 * KT; e += NT) {
+  for (int e = tid; e < NB * KT; e += NT) {
     half_t* kr = smem + (e / KT) * STAGE + (e % KT) * KLD;
-    for (int c = nch * 8; c < KLD; ++c) kr[c] = (half_t)0.0f;
+    for (int c = nch * 8; c < KLD; ++c) kr[c] = (half_t)((QSD > 0 && c == QSD) ? 1.0f : 0.0f);
     half_t* vr = smem + (e / KT) * STAGE + KS + (e % KT) * VLD;
     for (int c = nch * 8; c < VLD; ++c) vr[c] = (half_t)((ones_row && c == d) ? 1.0f : 0.0f);
   }
@@ -153,7 +156,11 @@ __global__ void __launch_bounds__(NW * 64, QB == 2 ? 1 : 2) attn_fwd_kernel(Attn
 #pragma unroll
     for (int i = 0; i < DV / 32; ++i) o[qb][i] = f16v{};
   // running max m (exp2 domain, per query row = per lane); the score chain is seeded with
-  // C = -m, so the MFMA emits s' = c*s - m and the common path is a bare v_exp per score
+  // C = -m, so the MFMA emits s' = c*s - m and the common path is a bare v_exp per score.
+  // QSD > 0 (d < DQK, d = QSD): -m rides in Q's padding column QSD against a column of ones in K
+  // instead (no 16-register seed, no seed moves per tile); m is then the fp16 value in Q, and
+  // every rescale uses the difference of those fp16 values, which softmax's shift invariance makes
+  // exact
   float m_run[QB], l_run[QB];
   f16v negm[QB];
 #pragma unroll
@@ -182,15 +189,13 @@ __global__ void __launch_bounds__(NW * 64, QB == 2 ? 1 : 2) attn_fwd_kernel(Attn
   if (NW == 8 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
 #endif
 
-  for (int t = 0; t < ntiles; ++t) {
-    const int cur = t & 1;
-    const half_t* Ks = smem + cur * STAGE;
-    const half_t* Vs = Ks + KS;
-    const int key0 = t * KT;
-
+  // the loop's four parts; s / pf are loop-carried so that the lagging half (STAG) can hold a
+  // tile's second score block and first P block across the barrier
+  f16v s[QB][2];
+  h8 pf[QB][4];
+  auto qk = [&](const half_t* Ks) __attribute__((always_inline)) {
     // S'^T = K (cQ)^T - m for two 32-key sub-blocks of every query block; each K fragment
     // is read once for all QB blocks
-    f16v s[QB][2];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
@@ -198,15 +203,33 @@ __global__ void __launch_bounds__(NW * 64, QB == 2 ? 1 : 2) attn_fwd_kernel(Attn
         const h8 a = *reinterpret_cast<const h8*>(Ks + (kb * 32 + fr) * KLD + ks * 16 + 8 * fh);
 #pragma unroll
         for (int qb = 0; qb < QB; ++qb)
-          s[qb][kb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, qf[qb][ks], ks == 0 ? negm[qb] : s[qb][kb], 0, 0, 0);
+          s[qb][kb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, qf[qb][ks], ks > 0 ? s[qb][kb] : QSD > 0 ? f16v{} : negm[qb], 0, 0, 0);
       }
-    // tile t+1 (in registers since last iteration) -> the other stage; then issue t+2
-    if (t + 1 < ntiles) {
-      stage(cur ^ 1);
-      if (t + 2 < ntiles) fetch(t + 2);
+  };
+  auto exp_block = [&](int kb) __attribute__((always_inline)) {
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb) {
+      float ls = 0.f;
+#pragma unroll
+      for (int hlf = 0; hlf < 2; ++hlf) {
+        h8 pk;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float e = fast_exp2(s[qb][kb][hlf * 8 + j]);
+          if (!ones_row) ls += e;
+          pk[j] = (half_t)e;
+        }
+        pf[qb][kb * 2 + hlf] = pk;
+      }
+      if (!ones_row) {
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(ls), __float_as_uint(ls), false, false);
+        l_run[qb] += __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+      }
     }
-
-    h8 pf[QB][4];
+  };
+  // mask, tile max, (rare) rescale, then P of the first 32-key block
+  auto softmax_a = [&](int t) __attribute__((always_inline)) {
+    const int key0 = t * KT;
 #pragma unroll
     for (int qb = 0; qb < QB; ++qb) {
       if constexpr (CAUSAL) {
@@ -240,7 +263,12 @@ __global__ void __launch_bounds__(NW * 64, QB == 2 ? 1 : 2) attn_fwd_kernel(Attn
       }
       // raise the running max only on the first tile or past the headroom (P <= 2^DEFER)
       if (t == 0 || __any(mt > DEFER)) {
-        const float dm = t == 0 ? mt : fmaxf(mt, 0.f);
+        float dm = t == 0 ? mt : fmaxf(mt, 0.f);
+        if constexpr (QSD > 0) {
+          const half_t mh = (half_t)(-(m_run[qb] + dm));
+          dm = -(float)mh - m_run[qb];
+          if (fh == ((QSD & 15) >> 3)) qf[qb][QSD >> 4][QSD & 7] = mh;
+        }
         const float alpha = fast_exp2(-dm);
         l_run[qb] *= alpha;
 #pragma unroll
@@ -252,31 +280,17 @@ __global__ void __launch_bounds__(NW * 64, QB == 2 ? 1 : 2) attn_fwd_kernel(Attn
 #pragma unroll
           for (int r = 0; r < 16; ++r) s[qb][kb][r] -= dm;
         m_run[qb] += dm;
+        if constexpr (QSD == 0) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) negm[qb][r] = -m_run[qb];
-      }
-      float ls = 0.f;
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int hlf = 0; hlf < 2; ++hlf) {
-          h8 pk;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float e = fast_exp2(s[qb][kb][hlf * 8 + j]);
-            if (!ones_row) ls += e;
-            pk[j] = (half_t)e;
-          }
-          pf[qb][kb * 2 + hlf] = pk;
+          for (int r = 0; r < 16; ++r) negm[qb][r] = -m_run[qb];
         }
-      if (!ones_row) {
-        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(ls), __float_as_uint(ls), false, false);
-        l_run[qb] += __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
       }
     }
-
-    // O^T += V^T P^T ; element j of lane half fh in k-step ks is key 16ks + 8(j>>2) + 4fh + (j&3);
-    // each V^T fragment (ds_read_b64_tr_b16 pair) is read once for all QB blocks
+    exp_block(0);
+  };
+  // O^T += V^T P^T ; element j of lane half fh in k-step ks is key 16ks + 8(j>>2) + 4fh + (j&3);
+  // each V^T fragment (ds_read_b64_tr_b16 pair) is read once for all QB blocks
+  auto pv = [&](const half_t* Vs) __attribute__((always_inline)) {
 #pragma unroll
     for (int db = 0; db < DV / 32; ++db) {
 #pragma unroll
@@ -291,7 +305,40 @@ __global__ void __launch_bounds__(NW * 64, QB == 2 ? 1 : 2) attn_fwd_kernel(Attn
         for (int qb = 0; qb < QB; ++qb) o[qb][db] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, pf[qb][ks], o[qb][db], 0, 0, 0);
       }
     }
-    __syncthreads();   // stage `cur` fully read before it is restaged; stage cur^1 visible
+  };
+
+  // STAG: waves NW/2.. run half a tile behind their SIMD partners (waves w and w + NW/2 share a
+  // SIMD): the lead half computes [QK_t | softmax_t | PV_t], the lag half [exp2_{t-1} | PV_{t-1}
+  // QK_t | max/exp1_t], so one wave's matrix phase meets the other's v_exp phase
+  // (MI355X_MICROARCH.md two-waves item 9).  Tile t-1's V stays in its stage for the lag half's
+  // PV during iteration t: three stages instead of two.
+  const bool lag = STAG && wave >= NW / 2;
+  int bcur = 0;
+  for (int t = 0; t < ntiles; ++t) {
+    const int bnext = bcur + 1 == NB ? 0 : bcur + 1;
+    const int bprev = bcur == 0 ? NB - 1 : bcur - 1;
+    const half_t* Ks = smem + bcur * STAGE;
+    if (lag && t > 0) {
+      exp_block(1);
+      pv(smem + bprev * STAGE + KS);
+    }
+    qk(Ks);
+    // tile t+1 (in registers since last iteration) -> its stage; then issue t+2
+    if (t + 1 < ntiles) {
+      stage(bnext);
+      if (t + 2 < ntiles) fetch(t + 2);
+    }
+    softmax_a(t);
+    if (!lag) {
+      exp_block(1);
+      pv(Ks + KS);
+    }
+    __syncthreads();   // stage t+1 visible; with two stages, stage t fully read before it is restaged
+    bcur = bnext;
+  }
+  if (lag && ntiles > 0) {
+    exp_block(1);
+    pv(smem + (bcur == 0 ? NB - 1 : bcur - 1) * STAGE + KS);
   }
 
 #pragma unroll
@@ -328,7 +375,7 @@ __global__ void __launch_bounds__(NW * 64, QB == 2 ? 1 : 2) attn_fwd_kernel(Attn
   }
 }
 
-template <int DQK, int DV, int NW, int QB>
+template <int DQK, int DV, int NW, int QB, bool STAG = false, int QSD = 0>
 int launch(const AttnParams& p, hipStream_t s) {
   constexpr int ROWS = 32 * QB * NW;
   const long long blocks = (long long)((p.nq + ROWS - 1) / ROWS) * p.heads * p.batch;
@@ -341,7 +388,7 @@ int launch(const AttnParams& p, hipStream_t s) {
     }
     return fail(SDK_EINVAL, "attention: causal needs the one-block-per-wave form");
   }
-  hipLaunchKernelGGL((attn_fwd_kernel<DQK, DV, NW, QB>), grid, dim3(NW * 64), 0, s, p);
+  hipLaunchKernelGGL((attn_fwd_kernel<DQK, DV, NW, QB, false, STAG, QSD>), grid, dim3(NW * 64), 0, s, p);
   return check_launch("attn_fwd");
 }
 
@@ -376,9 +423,17 @@ extern "C" int sdk_attention(const sdk_attention_args* a, sdk_stream_t stream) {
   // 547 vs 623 us for the 4-wave form at SD-1's 64x64 level); SDK_ATTN_NW=4 selects the latter.
   // d = 160 keeps 4 waves: at 256 query rows one 8-wave group per head would idle half the CUs
   static const int nw4 = getenv("SDK_ATTN_NW") && atoi(getenv("SDK_ATTN_NW")) == 4;
-  if (d <= 48) return qb2 ? launch<48, 64, 4, 2>(p, s) : nw4 ? launch<48, 64, 4, 1>(p, s) : launch<48, 64, 8, 1>(p, s);
-  if (d <= 64) return nw4 ? launch<64, 64, 4, 1>(p, s) : launch<64, 64, 8, 1>(p, s);
-  if (d <= 80) return nw4 ? launch<80, 96, 4, 1>(p, s) : launch<80, 96, 8, 1>(p, s);   // 165 vs 189 VGPRs
+  // SDK_ATTN_STAG=1: the 8-wave forms with the lag half staggered by half a tile (three stages)
+  static const int stag = getenv("SDK_ATTN_STAG") && atoi(getenv("SDK_ATTN_STAG")) == 1;
+  if (d <= 48)
+    return qb2 ? launch<48, 64, 4, 2>(p, s)
+           : nw4  ? launch<48, 64, 4, 1>(p, s)
+           : d == 40 ? (stag ? launch<48, 64, 8, 1, true, 40>(p, s) : launch<48, 64, 8, 1, false, 40>(p, s))
+           : stag ? launch<48, 64, 8, 1, true>(p, s) : launch<48, 64, 8, 1>(p, s);
+  if (d <= 64)
+    return nw4 ? launch<64, 64, 4, 1>(p, s) : stag ? launch<64, 64, 8, 1, true>(p, s) : launch<64, 64, 8, 1>(p, s);
+  if (d <= 80)   // 165 vs 189 VGPRs
+    return nw4 ? launch<80, 96, 4, 1>(p, s) : stag ? launch<80, 96, 8, 1, true>(p, s) : launch<80, 96, 8, 1>(p, s);
   if (d <= 96) return launch<96, 96, 4, 1>(p, s);
   if (d <= 128) return launch<128, 128, 4, 1>(p, s);
   return launch<160, 160, 4, 1>(p, s);

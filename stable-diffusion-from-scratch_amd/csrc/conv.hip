@@ -50,6 +50,7 @@ struct Params {
   int M, N, Npad, batch, ho, wo, hw_out;
   const half_t* W;
   int ldw, wrows;       // packed weight rows (>= N); reads beyond are clamped
+  long long wbs;        // per-image weights: W of image b at W + b * wbs (0: one W); LDS-DMA kernels only
   const float* bias;
   const float* row_bias;
   int rb_ld;
@@ -1074,7 +1075,7 @@ struct DmaSrc {
   __amdgpu_buffer_rsrc_t a0, a1, s0, s1, w;
 };
 
-__device__ __forceinline__ DmaSrc make_dma_src(const Params& p) {
+__device__ __forceinline__ DmaSrc make_dma_src(const Params& p, int m0) {
   const Seg& g0 = p.seg[0];
   const Seg& g1 = p.seg[1];
   const long long npix0 = (long long)p.batch * g0.h * g0.w;
@@ -1084,7 +1085,8 @@ __device__ __forceinline__ DmaSrc make_dma_src(const Params& p) {
   d.a1 = ph_rsrc(g0.src1 ? g0.src1 : g0.src0, npix0 * (g0.src1 ? g0.ld1 : g0.ld0) * 2);
   d.s0 = ph_rsrc(two ? g1.src0 : g0.src0, two ? (long long)p.M * g1.ld0 * 2 : 0);
   d.s1 = ph_rsrc(two && g1.src1 ? g1.src1 : g0.src0, two && g1.src1 ? (long long)p.M * g1.ld1 * 2 : 0);
-  d.w = ph_rsrc(p.W, (long long)p.wrows * p.ldw * 2);
+  // per-image weights: an M-tile lies inside one image (planner), so one base per workgroup
+  d.w = ph_rsrc(p.wbs ? p.W + (size_t)(m0 / p.hw_out) * p.wbs : p.W, (long long)p.wrows * p.ldw * 2);
   return d;
 }
 
@@ -1225,7 +1227,7 @@ __global__ void __launch_bounds__(CF::NT, CF::OCC * CF::NW / 4) conv_glds_kernel
   const int m0 = tm * CF::TBM, n0 = tn * CF::TBN;
   const int kt0 = sidx * p.kt_per_split, kt1 = min(p.kt_total, kt0 + p.kt_per_split);
   const int lrow = lane >> 3;
-  const DmaSrc d = make_dma_src(p);
+  const DmaSrc d = make_dma_src(p, m0);
   // per piece j (rows (j*NW + wave)*8 + lrow of the stage): A -> (pixb, msk), W -> byte offset
   unsigned cx[GPW], cy[GPW];
 #pragma unroll
@@ -1479,7 +1481,7 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_halo_kernel(Params p)
   const int lrow = lane >> 3;
   const Seg& g0 = p.seg[0];
   const Seg& g1 = p.seg[1];
-  const DmaSrc d = make_dma_src(p);
+  const DmaSrc d = make_dma_src(p, m0);
   const int NP = p.h_np, RP = p.h_rp, HS = p.h_hs;
   half_t* const halo = lds + 2 * CF::WSTAGE_H;
   // the tile's halo: whole padded rows from the first output row it touches (whole images when a
@@ -1919,7 +1921,7 @@ __global__ void __launch_bounds__(512) conv_ph_kernel(Params p) {
   const int lrow = lane >> 3;
   const int rch = (lane & 7) ^ ((wave * 4 + (lrow >> 1)) & 7);
 
-  const DmaSrc d = make_dma_src(p);
+  const DmaSrc d = make_dma_src(p, m0);
   const EpiVec ev = epi_vec_load(p, m0, n0, 256, 256);
   // this lane's DMA rows: slot row j*64 + wave*8 + lrow of every half (q = half*2 + j)
   unsigned pixb[4], msk[4], wv[4];
@@ -2632,6 +2634,9 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   if (a->out_mode == SDK_OUT_GEGLU_F16 && (a->cout % 64)) return fail(SDK_EINVAL, "conv2d: GEGLU cout % 64");
   p.kt_total = kt;
   p.W = (const half_t*)a->weight; p.ldw = a->k_total; p.wrows = (a->cout + 127) / 128 * 128;
+  p.wbs = a->weight_batch_stride;
+  if (p.wbs < 0 || (p.wbs && p.wbs < (long long)p.wrows * p.ldw))
+    return fail(SDK_EINVAL, "conv2d: weight_batch_stride smaller than one packed weight matrix");
   p.bias = a->bias; p.row_bias = a->row_bias; p.rb_ld = a->row_bias_ld;
   p.res = (const half_t*)a->residual; p.res_ld = a->res_ld;
   p.out = a->out; p.out_ld = a->out_ld; p.out_mode = a->out_mode;
@@ -2677,10 +2682,12 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
     fill = bf;
     return best;
   };
+  if (p.wbs && transform) return fail(SDK_EINVAL, "conv2d: per-image weights need a transform-free operand");
   if (!transform) {
     double best = -1;
     for (const Opt& o : opts) {
       if (a->out_mode == SDK_OUT_GEGLU_F16 && !o.geglu_ok) continue;
+      if (p.wbs && p.hw_out % o.bm) continue;   // per-image weights: M-tiles inside one image
       const int tmm = (p.M + o.bm - 1) / o.bm, tnn = (p.N + o.bn - 1) / o.bn;
       const double eff = (double)p.M * p.N / ((double)tmm * o.bm * tnn * o.bn);
       double fill;
@@ -2704,7 +2711,7 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
     const bool direct_ok = a->nseg == 1 && a->cout <= DC_MAXN && (g.ksize == 3 || (g.ksize == 1 && g.pad == 0)) &&
                            g.stride == 1 && !g.upsample && g.pad_end == 0 && g.pad <= 1 && g.c_split == g.cin &&
                            g.gn_scale == nullptr && !g.silu && !a->residual && !a->row_bias &&
-                           a->act == SDK_ACT_NONE && a->out_mode != SDK_OUT_GEGLU_F16;
+                           a->act == SDK_ACT_NONE && a->out_mode != SDK_OUT_GEGLU_F16 && !p.wbs;
     if (forced == 34 && !direct_ok) return fail(SDK_EINVAL, "conv2d: variant 34 (direct) does not fit this conv");
     if (direct_ok && (forced < 0 || forced == 34)) {
       p.variant = 34;
@@ -2729,7 +2736,8 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
     const sdk_conv_src& g = a->seg[0];
     const bool skinny_ok = a->nseg == 1 && p.M <= SK_MAXM && g.ksize == 1 && g.stride == 1 && g.pad == 0 &&
                            g.pad_end == 0 && !g.upsample && g.c_split == g.cin && g.gn_scale == nullptr &&
-                           (a->out_mode == SDK_OUT_NHWC_F16 || a->out_mode == SDK_OUT_ROWS_F32) && !a->gn_partial;
+                           (a->out_mode == SDK_OUT_NHWC_F16 || a->out_mode == SDK_OUT_ROWS_F32) && !a->gn_partial &&
+                           !p.wbs;
     if (forced == 35 && !skinny_ok) return fail(SDK_EINVAL, "conv2d: variant 35 (skinny) does not fit this GEMM");
     if (skinny_ok && (forced < 0 || forced == 35)) {
       p.variant = 35;
@@ -2765,7 +2773,7 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
     const int nw = v == 36 ? HCfg256x320::NW : HCfg128x320::NW;
     const int max_rp = v == 36 ? HCfg256x320::MAX_RP : HCfg128x320::MAX_RP;
     const bool common = seg1_ok && g.ksize == 3 && g.stride == 1 && g.pad_end == 0 && !g.upsample &&
-                        a->out_mode != SDK_OUT_GEGLU_F16;
+                        a->out_mode != SDK_OUT_GEGLU_F16 && !p.wbs;
     // physical: a pad-0 conv over a zero-bordered input; virtual (GroupNorm-fused): a pad-1 conv over the
     // raw input with its GroupNorm scale / shift (+ SiLU), whole 64-channel blocks, single-image tiles
     const bool phys_ok = common && !transform && g.pad == 0 && p.nomask;
@@ -2859,11 +2867,15 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
                                 256, 128, 128, 256, 256, 256, 128, 256, 128, 128, 256, 256, 256, 256, 128, 128, 128};
     static const int fbn[34] = {128, 0, 256, 128, 128, 320, 160, 320, 256, 256, 256, 256, 256, 256, 256, 256, 128,
                                 128, 128, 256, 256, 256, 320, 320, 160, 256, 128, 256, 256, 256, 256, 160, 128, 160};
-    var = forced;
-    tbm = fbm[fbase];
-    tbn = fbn[fbase];
-    best_split = 0;
+    if (!p.wbs || (forced != 0 && p.hw_out % fbm[fbase] == 0)) {
+      var = forced;
+      tbm = fbm[fbase];
+      tbn = fbn[fbase];
+      best_split = 0;
+    }
   }
+  if (p.wbs && (var == 0 || p.hw_out % tbm))
+    return fail(SDK_EINVAL, "conv2d: per-image weights: no LDS-DMA tile fits inside one image");
   p.variant = var;
   p.tiles_m = (p.M + tbm - 1) / tbm;
   p.tiles_n = (p.N + tbn - 1) / tbn;

@@ -311,13 +311,13 @@ __global__ void __launch_bounds__(256, 1) xattn_block_kernel(XAttnParams p) {
     h4v pf[HPI][XKP / 16];
 #pragma unroll
     for (int g = 0; g < HPI; ++g) {
-      mx[g] = -INFINITY;
+      mx[g] = -__builtin_inff();
 #pragma unroll
       for (int kb = 0; kb < XKP / 16; ++kb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = 16 * kb + 4 * c16 + r;
-          const float v = key < p.nk ? s[g][kb][r] * p.c : -INFINITY;
+          const float v = key < p.nk ? s[g][kb][r] * p.c : -__builtin_inff();
           s[g][kb][r] = v;
           mx[g] = fmaxf(mx[g], v);
         }
@@ -431,6 +431,41 @@ int launch_xattn(const XAttnParams& p, int m, hipStream_t s) {
   return check_launch("xattn_block");
 }
 
+// Segment softmax of the reassociated cross-attention (1280-channel levels, attention.py:106-112
+// rearranged): row m of s holds, for every head h, the 77 scores of its query against the context
+// keys in columns [h*seglen, (h+1)*seglen); p = softmax over each segment of scale*s, fp16, with the
+// columns from nseg*seglen up to the row's K padding written as zeros.  One wave per row, one
+// segment at a time: 64 + 64 columns per lane pair, a DPP max and sum per segment.
+__device__ __forceinline__ float wave_max_f(float x) {
+  x = fmaxf(x, dpp_f<0xB1>(x));
+  x = fmaxf(x, dpp_f<0x4E>(x));
+  x = fmaxf(x, dpp_f<0x124>(x));
+  x = fmaxf(x, dpp_f<0x128>(x));
+  return fmaxf(fmaxf(readlane_f(x, 0), readlane_f(x, 16)), fmaxf(readlane_f(x, 32), readlane_f(x, 48)));
+}
+
+__global__ void __launch_bounds__(256) segment_softmax_kernel(const float* __restrict__ s, int ld_s,
+                                                               half_t* __restrict__ p, int ld_p, int rows, int nseg,
+                                                               int seglen, float c) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* sr = s + (size_t)row * ld_s;
+  half_t* pr = p + (size_t)row * ld_p;
+  for (int h = 0; h < nseg; ++h) {
+    const int c0 = h * seglen + lane, c1 = c0 + 64;
+    const bool ok0 = lane < seglen, ok1 = lane + 64 < seglen;
+    const float x0 = ok0 ? sr[c0] : -__builtin_inff(), x1 = ok1 ? sr[c1] : -__builtin_inff();
+    const float m = wave_max_f(fmaxf(x0, x1));
+    const float e0 = ok0 ? __builtin_amdgcn_exp2f((x0 - m) * c) : 0.f;
+    const float e1 = ok1 ? __builtin_amdgcn_exp2f((x1 - m) * c) : 0.f;
+    const float inv = 1.f / wave_sum_f(e0 + e1);
+    if (ok0) pr[c0] = (half_t)(e0 * inv);
+    if (ok1) pr[c1] = (half_t)(e1 * inv);
+  }
+  for (int col = nseg * seglen + lane; col < ld_p; col += 64) pr[col] = (half_t)0.f;
+}
+
 }  // namespace
 }  // namespace sdk
 
@@ -492,4 +527,16 @@ extern "C" int sdk_cross_attention_block_ln(const sdk_xattn_args* a, const sdk_x
                                             sdk_stream_t stream) {
   if (!ln) return fail(SDK_EINVAL, "cross_attention_block_ln: null norm arguments");
   return xattn_run(a, ln, stream);
+}
+
+extern "C" int sdk_segment_softmax(const float* s, int32_t ld_s, void* p, int32_t ld_p, int32_t rows, int32_t nseg,
+                                   int32_t seglen, float scale, sdk_stream_t stream) {
+  if (!s || !p) return fail(SDK_EINVAL, "segment_softmax: null pointer");
+  if (rows <= 0 || nseg <= 0 || seglen <= 0 || seglen > 128)
+    return fail(SDK_EINVAL, "segment_softmax: rows / nseg must be positive, 1 <= seglen <= 128");
+  if (ld_s < nseg * seglen || ld_p < nseg * seglen) return fail(SDK_EINVAL, "segment_softmax: row stride too small");
+  const int blocks = (rows + 3) / 4;
+  hipLaunchKernelGGL(segment_softmax_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, s, ld_s, (half_t*)p,
+                     ld_p, rows, nseg, seglen, scale * 1.4426950408889634f);
+  return check_launch("segment_softmax");
 }

@@ -80,8 +80,44 @@ def _use_fused_xattn(channels, head_dim, nk, n_img, batch):
     return ops.cross_attention_block_supported(channels, head_dim, nk, n_img)
 
 
+# Reassociated cross-attention where the heads x context columns are fewer than the channels (SD-1's
+# 1280-channel levels: 8 x 77 = 616 -> 640 vs 1280): per prompt b and head h, K_h Wq_h (77 x C) and
+# Wo_h V_h^T (C x 77) are precomputed with the context K|V, so the per-step block is
+#   s = t [K_h Wq_h]_h^T (one GEMM, N = H*77) -> p = segment softmax(scale s) -> out = p [Wo_h V_h^T]_h^T + b + x
+# — 4*M*C*H*77 FLOP instead of 4*M*C*(C + 77) (2.1x fewer at 1280), the same math as
+# softmax(q K^T) V Wo^T with q = t Wq^T (reference attention.py:96-117).  SD_AMD_XATTN_REASSOC=0 keeps
+# the three launches.
+XATTN_REASSOC = os.environ.get("SD_AMD_XATTN_REASSOC") != "0"
+
+
+class ReassocContext:
+    """A prompt batch's cross-attention operands: the K|V projection (the three-launch path) and the
+    per-prompt reassociated GEMM weights."""
+    __slots__ = ("kv", "w1", "w2", "heads", "nk")
+
+    def __init__(self, kv, w1, w2, heads, nk):
+        self.kv, self.w1, self.w2, self.heads, self.nk = kv, w1, w2, heads, nk
+
+
+def reassoc_weights(k, v, wq, wo):
+    """fp32 per-prompt matrices of the reassociated block: k, v [B, L, H, d] (the context K / V),
+    wq [H*d, C] (to_q.weight), wo [Co, H*d] (to_out.weight) -> w1 [B, H*L, C] with
+    w1[b, h*L + j] = K[b, j, h] Wq_h, and w2 [B, Co, H*L] with w2[b, :, h*L + j] = Wo_h V[b, j, h]^T."""
+    B, L, H, d = k.shape
+    w1 = torch.einsum("bjhe,hec->bhjc", k, wq.view(H, d, -1)).reshape(B, H * L, -1)
+    w2 = torch.einsum("che,bjhe->bchj", wo.view(wo.shape[0], H, d), v).reshape(B, wo.shape[0], H * L)
+    return w1, w2
+
+
+def _reassoc_applies(inner, heads, nk):
+    kr = (heads * nk + ops.BK - 1) // ops.BK * ops.BK
+    return XATTN_REASSOC and 2 * kr <= inner
+
+
 class CrossAttention(nn.Module):
-    """Reference ``attention.py:24-117``: no-bias q/k/v, to_out Linear+Dropout, scale d^-1/2."""
+    """Reference ``attention.py:24-117``: no-bias q/k/v, to_out Linear+Dropout, scale d^-1/2.
+    At the 1280-channel levels with a cached context the per-step block runs reassociated
+    (``ReassocContext``)."""
 
     def __init__(self, query_dim, context_dim=None, heads=8, dim_head=64, dropout=0.):
         super().__init__()
@@ -106,10 +142,30 @@ class CrossAttention(nn.Module):
         self._pc_kv = ops.PackedConv([(torch.cat([self.to_k.weight, self.to_v.weight], 0), cd)], None, device=dev)
         self._pc_o = ops.PackedConv([(self.to_out[0].weight, self.heads * self.dim_head)], self.to_out[0].bias,
                                     device=dev)
+        if not self.self_attn:
+            self._wq32 = self.to_q.weight.detach().to(dev, torch.float32)          # [inner, C]
+            self._wo32 = self.to_out[0].weight.detach().to(dev, torch.float32)     # [C, inner]
+            self._bo32 = self.to_out[0].bias.detach().to(dev, torch.float32).contiguous()
 
-    def context_kv(self, ctx2d):
-        """K|V of the conditioning, [B*L, 2*inner] — computed once per conditioning tensor."""
-        return ops.linear(self._pc_kv, ctx2d)
+    def context_kv(self, ctx2d, L=None):
+        """K|V of the conditioning, [B*L, 2*inner] — computed once per conditioning tensor; with ``L``
+        (context tokens) and a shape where it pays, wrapped with the reassociated per-prompt weights."""
+        kv = ops.linear(self._pc_kv, ctx2d)
+        inner = self.heads * self.dim_head
+        if L is None or self.self_attn or not _reassoc_applies(inner, self.heads, L):
+            return kv
+        B, H, d = ctx2d.shape[0] // L, self.heads, self.dim_head
+        C = self.to_q.in_features
+        Co = self.to_out[0].out_features
+        kr = (H * L + ops.BK - 1) // ops.BK * ops.BK
+        k = kv[:, :inner].float().view(B, L, H, d)
+        v = kv[:, inner:].float().view(B, L, H, d)
+        r1, r2 = reassoc_weights(k, v, self._wq32, self._wo32)
+        w1 = torch.zeros(B, (kr + ops.BN - 1) // ops.BN * ops.BN, C, dtype=torch.float16, device=kv.device)
+        w1[:, :H * L] = r1.half()
+        w2 = torch.zeros(B, (Co + ops.BN - 1) // ops.BN * ops.BN, kr, dtype=torch.float16, device=kv.device)
+        w2[:, :Co, :H * L] = r2.half()
+        return ReassocContext(kv, ops.PerImageWeights(w1, H * L), ops.PerImageWeights(w2, Co, self._bo32), H, L)
 
     def _run(self, t, residual, B, N, kv=None, Lc=None):
         inner = self.heads * self.dim_head
@@ -126,6 +182,14 @@ class CrossAttention(nn.Module):
             # the per-step block the bench reports (``cross_attention_block``); one fused kernel
             # where the shape is supported, else the three launches
             ops.PROFILER.region = "cross_attention"
+            if isinstance(kv, ReassocContext):
+                if t.stride(-1) == 1 and N % 128 == 0 and kv.w1.weight.shape[0] == B:
+                    s = ops.linear(kv.w1, t, out_mode=ops.OUT_ROWS_F32, n_img=N)
+                    p = ops.segment_softmax(s, kv.heads, kv.nk, self.scale, ld_p=kv.w2.k_total)
+                    out = ops.linear(kv.w2, p, residual=residual, n_img=N)
+                    ops.PROFILER.region = None
+                    return out
+                kv = kv.kv
             if t.stride(-1) == 1 and _use_fused_xattn(inner, self.dim_head, Lc, N, B):
                 out = ops.cross_attention_block(t, kv, self._pc_q, self._pc_o, batch=B, n_img=N, nk=Lc,
                                                 heads=self.heads, head_dim=self.dim_head, scale=self.scale,
@@ -231,8 +295,8 @@ class SpatialTransformer(nn.Module):
         for blk in self.transformer_blocks:
             blk._prepare(dev)
 
-    def context_kv(self, ctx2d):
-        return [blk.attn2.context_kv(ctx2d) for blk in self.transformer_blocks]
+    def context_kv(self, ctx2d, L=None):
+        return [blk.attn2.context_kv(ctx2d, L) for blk in self.transformer_blocks]
 
     def _run(self, x, kvs=None, Lc=None):
         B, H, W, Cc = x.shape

@@ -345,7 +345,7 @@ class UNetModel(nn.Module):
             c2 = ops.nchw_to_nhwc(context.reshape(B * L, D, 1, 1).float(), D).view(B * L, D)
         kv = {}
         for st in self._sts:
-            kv[id(st)] = st.context_kv(c2)
+            kv[id(st)] = st.context_kv(c2, L)
         self._ctx_cache[id(context)] = (context, context._version, kv)
         self._ctx_cache.move_to_end(id(context))
         while len(self._ctx_cache) > self.CONTEXT_CACHE_SIZE:

@@ -186,6 +186,24 @@ class PackedConv:
         self.bias = b.to(device=device, dtype=torch.float32).contiguous() if b is not None else None
 
 
+class PerImageWeights:
+    """Per-image GEMM weights for ``linear(..., n_img=)``: ``weight`` fp16 [batch, n_pad, k] (row n of
+    image b's matrix, K contiguous; n_pad = roundup(n, 128)), so output rows of image b use matrix b
+    (``sdk_conv_args.weight_batch_stride``).  The reassociated cross-attention's per-prompt K_h Wq_h and
+    Wo_h V_h^T (openai_model/attention.py)."""
+
+    def __init__(self, weight, n, bias=None):
+        assert weight.dim() == 3 and weight.dtype == torch.float16 and weight.is_contiguous()
+        assert weight.shape[1] % BN == 0 and weight.shape[2] % BK == 0 and n <= weight.shape[1]
+        self.weight = weight
+        self.N = n
+        self.k_total = weight.shape[2]
+        self.bias = bias
+        self.geglu = False
+        self.seg_geom = [(1, weight.shape[2])]
+        self.w_batch_stride = weight.shape[1] * weight.shape[2]
+
+
 def _conv_source_hash():
     import hashlib
     import os
@@ -240,7 +258,7 @@ class _Autotune:
         s0, s1 = a.seg[0], a.seg[1]
         return (a.batch, a.ho, a.wo, a.cout, a.nseg, pc.k_total, a.out_mode, s0.cin, s0.h, s0.w, s0.ksize,
                 s0.stride, s0.upsample, s0.c_split, int(bool(s0.gn_scale) or bool(s0.silu)),
-                s1.cin if a.nseg > 1 else 0, int(gn))
+                s1.cin if a.nseg > 1 else 0, int(gn), int(bool(a.weight_batch_stride)))
 
     def choose(self, a, pc, dev, gn=False):
         """``gn``: the output feeds a GroupNorm — candidates are timed emitting the statistics, and
@@ -417,6 +435,7 @@ def conv2d(pc: PackedConv, x, *, ksize=None, stride=1, pad=None, pad_end=0, upsa
     a.act = act
     a.weight = pc.weight.data_ptr()
     a.k_total = pc.k_total
+    a.weight_batch_stride = getattr(pc, "w_batch_stride", 0)
     a.bias = pc.bias.data_ptr() if (bias and pc.bias is not None) else None
     if row_bias is not None:
         rb, off = row_bias
@@ -477,18 +496,37 @@ def conv2d(pc: PackedConv, x, *, ksize=None, stride=1, pad=None, pad_end=0, upsa
 
 
 def linear(pc: PackedConv, x2d, *, silu=False, residual=None, out_mode=OUT_NHWC_F16, out=None, bias=True,
-           act=ACT_NONE):
+           act=ACT_NONE, n_img=None):
     """Token GEMM: x2d [M, K] fp16 → [M, N]; a 1x1 conv over an M x 1 image.  ``silu`` applies to
-    the input (prologue), ``act`` to the output (epilogue, before the residual)."""
+    the input (prologue), ``act`` to the output (epilogue, before the residual).  ``n_img``: rows per
+    image, for a ``PerImageWeights`` pc (the GEMM runs as M / n_img images of n_img x 1)."""
     _claim(out)
     M = x2d.shape[0]
-    x4 = x2d.view(1, M, 1, x2d.shape[-1]) if x2d.stride(-1) == 1 and x2d.is_contiguous() else None
+    nb, rows = (1, M) if n_img is None else (M // n_img, n_img)
+    assert nb * rows == M
+    if isinstance(pc, PerImageWeights):
+        assert n_img is not None and nb == pc.weight.shape[0], "per-image weights: n_img must split M by image"
+    x4 = x2d.view(nb, rows, 1, x2d.shape[-1]) if x2d.stride(-1) == 1 and x2d.is_contiguous() else None
     if x4 is None:
-        x4 = x2d.as_strided((1, M, 1, x2d.shape[1]), (0, x2d.stride(0), x2d.stride(0), 1))
-    res4 = residual.view(1, M, 1, residual.shape[-1]) if residual is not None else None
+        x4 = x2d.as_strided((nb, rows, 1, x2d.shape[1]), (rows * x2d.stride(0), x2d.stride(0), x2d.stride(0), 1))
+    res4 = residual.view(nb, rows, 1, residual.shape[-1]) if residual is not None else None
     y = conv2d(pc, x4, ksize=1, pad=0, silu=silu, residual=res4, out_mode=out_mode, bias=bias,
-               out=None if out is None else out.view(1, M, 1, out.shape[-1]), act=act)
+               out=None if out is None else out.view(nb, rows, 1, out.shape[-1]), act=act)
     return y.view(M, y.shape[-1])
+
+
+def segment_softmax(s, nseg, seglen, scale, ld_p=None, out=None):
+    """p = softmax over each of the ``nseg`` ``seglen``-column segments of scale * s (fp32 [M, ld] →
+    fp16 [M, ld_p], columns from nseg*seglen zero): the reassociated cross-attention's softmax."""
+    _need_cuda(s, "segment_softmax")
+    assert s.dtype == torch.float32 and s.stride(-1) == 1
+    M = s.shape[0]
+    ld_p = ld_p or (nseg * seglen + BK - 1) // BK * BK
+    if out is None:
+        out = torch.empty(M, ld_p, dtype=torch.float16, device=s.device)
+    check(lib().sdk_segment_softmax(s.data_ptr(), s.stride(0), out.data_ptr(), out.stride(0), M, nseg, seglen,
+                                    float(scale), _stream()), "segment_softmax")
+    return out
 
 
 # --------------------------------------------------------------------------- normalisation

@@ -123,8 +123,43 @@ def phases():
               "  ".join(f"{n} {v:5.1f}" for n, v in zip(names, d.mean(0).tolist())), flush=True)
 
 
+def reassoc():
+    """The 1280-channel block (sd1_16x16: B=16, 256 tokens; and its CFG batch): reassociated (per-prompt
+    K_h Wq_h / Wo_h V_h^T GEMMs around a segment softmax) vs the three launches, through the model's own
+    CrossAttention._run, both autotuned; prints the two timings and their rel-L2 difference."""
+    import sd_amd_loader
+    sd_amd_loader.load()
+    from sd_amd import ops
+    from sd_amd.openai_model.attention import CrossAttention, ReassocContext
+    ops.AUTOTUNE.enable(True)
+    torch.manual_seed(0)
+    for name, B, N in (("sd1_16x16", 16, 256), ("sd1_16x16_cfg", 32, 256)):
+        C, D, H, L = 1280, 160, 8, 77
+        att = CrossAttention(query_dim=C, context_dim=768, heads=H, dim_head=D).cuda()
+        with torch.no_grad():
+            for m in (att.to_q, att.to_k, att.to_v, att.to_out[0]):
+                m.weight.normal_(0, m.in_features ** -0.5)
+        att._prepare(torch.device("cuda"))
+        ctx = torch.randn(B * L, 768, device="cuda").half()
+        kvr = att.context_kv(ctx, L)
+        assert isinstance(kvr, ReassocContext)
+        t = torch.randn(B * N, C, device="cuda").half()
+        res = torch.randn(B * N, C, device="cuda").half()
+        f_re = lambda: att._run(t, res, B, N, kvr, L)
+        f_3 = lambda: att._run(t, res, B, N, kvr.kv, L)
+        y_re, y_3 = f_re(), f_3()
+        err = ((y_re.float() - y_3.float()).norm() / (y_3.float() - res.float()).norm()).item()
+        t_re, t_3 = timeit(f_re), timeit(f_3)
+        fl3 = 4.0 * B * N * C * C + 4.0 * B * N * L * C
+        print(f"{name:16s} B={B:3d} N={N:5d} C={C}  reassociated {t_re:8.1f} us   three launches {t_3:8.1f} us "
+              f"({fl3 / t_3 / 1e6:6.1f} TFLOP/s)  speedup {t_3 / t_re:5.2f}x  rel-L2(reassoc - three) of the "
+              f"block's update {err:.2e}", flush=True)
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "--phases":
         phases()
+    elif len(sys.argv) > 1 and sys.argv[1] == "--reassoc":
+        reassoc()
     else:
         main()
