@@ -265,6 +265,29 @@ int sdk_cross_attention_block_ln(const sdk_xattn_args* a, const sdk_xattn_ln_arg
 int sdk_segment_softmax(const float* s, int32_t ld_s, void* p, int32_t ld_p, int32_t rows, int32_t nseg,
                         int32_t seglen, float scale, sdk_stream_t stream);
 
+/* ---------------------------------------------------------------- fused feed-forward
+ * out[m] = res[m] + W2 (a * gelu(g)) + b2,  [a | g] = t[m] W1^T + b1  — the GEGLU FeedForward of
+ * BasicTransformerBlock in ONE kernel (GEGLU -> Dropout(0) -> Linear, openai_model/attention.py:129-172,
+ * called as x = self.ff(self.norm3(x)) + x at :253); the 4*channels-wide intermediate stays in registers.
+ * Shapes: channels == 320 (SD's 64x64-level blocks), features (the GEGLU width, 4*channels in SD) a
+ * multiple of 32 (sdk_ff_supported).  t / res / out: [rows, ld] fp16, 16-B aligned, ld % 8 == 0; res may
+ * be NULL or alias out.  Weights go through a one-time pack: w1 fp16 [2*features][channels] (rows
+ * [0, features) = a, [features, 2*features) = gate, as nn.Linear(channels, 2*features).weight), b1 fp32
+ * [2*features] or NULL, w2 fp16 [channels][features] (nn.Linear(features, channels).weight) ->
+ * `packed` (sdk_ff_packed_bytes bytes, 16-B aligned, device); b2 fp32 [channels] (16-B aligned) or NULL.
+ */
+typedef struct {
+  const void* t; const void* res; void* out; const void* packed; const float* b2;
+  int32_t t_ld, res_ld, out_ld;
+  int32_t rows, channels, features;
+} sdk_ff_args;
+
+int sdk_ff_supported(int32_t channels, int32_t features);
+int64_t sdk_ff_packed_bytes(int32_t channels, int32_t features);
+int sdk_ff_pack(const void* w1, const float* b1, const void* w2, void* packed, int32_t channels, int32_t features,
+                sdk_stream_t stream);
+int sdk_feed_forward(const sdk_ff_args* a, sdk_stream_t stream);
+
 /* ---------------------------------------------------------------- sampler / glue
  * DDIM update (DDIM/ddim.py:194-204 == ldm/diffusion/ddim.py:197-205), fp32,
  * evaluated op by op without contraction so it is bit-identical to torch's CPU

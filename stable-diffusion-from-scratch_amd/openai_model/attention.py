@@ -89,6 +89,10 @@ def _use_fused_xattn(channels, head_dim, nk, n_img, batch):
 # the three launches.
 XATTN_REASSOC = os.environ.get("SD_AMD_XATTN_REASSOC") != "0"
 
+# The 320-channel GEGLU FeedForward as one kernel (ops.feed_forward: the 4C intermediate stays in
+# registers); SD_AMD_FUSED_FF=0 keeps the two GEMMs.
+FUSED_FF = os.environ.get("SD_AMD_FUSED_FF") != "0"
+
 
 class ReassocContext:
     """A prompt batch's cross-attention operands: the K|V projection (the three-launch path) and the
@@ -227,8 +231,14 @@ class FeedForward(nn.Module):
         p = self.net[0].proj
         self._pc1 = ops.PackedConv([(p.weight, p.in_features)], p.bias, geglu=True, device=dev)
         self._pc2 = ops.PackedConv([(self.net[2].weight, self.net[2].in_features)], self.net[2].bias, device=dev)
+        self._pff = None
+        if FUSED_FF and ops.ff_supported(p.in_features, p.out_features // 2):
+            self._pff = ops.PackedFF(p.weight, p.bias, self.net[2].weight, self.net[2].bias, dev)
 
     def _run(self, t, residual):
+        if self._pff is not None and t.stride(-1) == 1:
+            # GEGLU GEMM -> GEGLU -> output GEMM -> + residual in one kernel (320 channels)
+            return ops.feed_forward(self._pff, t, residual=residual)
         g = ops.linear(self._pc1, t, out_mode=ops.OUT_GEGLU_F16)
         return ops.linear(self._pc2, g, residual=residual)
 

@@ -15,7 +15,7 @@ import math
 import torch
 
 from . import _lib
-from ._lib import (ACT_NONE, ACT_QUICK_GELU, AttentionArgs, XAttnArgs, XAttnLnArgs, ConvArgs, ConvPlanInfo, DdimArgs, GroupNormArgs,
+from ._lib import (ACT_NONE, ACT_QUICK_GELU, AttentionArgs, XAttnArgs, XAttnLnArgs, FfArgs, ConvArgs, ConvPlanInfo, DdimArgs, GroupNormArgs,
                    OUT_GEGLU_F16, OUT_NCHW_F32, OUT_NHWC_F16, OUT_ROWS_F32, check, lib)
 
 BK = 64          # K tile of the conv kernel (packed weight column padding)
@@ -518,7 +518,7 @@ def linear(pc: PackedConv, x2d, *, silu=False, residual=None, out_mode=OUT_NHWC_
 def segment_softmax(s, nseg, seglen, scale, ld_p=None, out=None):
     """p = softmax over each of the ``nseg`` ``seglen``-column segments of scale * s (fp32 [M, ld] →
     fp16 [M, ld_p], columns from nseg*seglen zero): the reassociated cross-attention's softmax."""
-    _need_cuda(s, "segment_softmax")
+    _need_cuda(s, "segment_softmax", torch.float32)
     assert s.dtype == torch.float32 and s.stride(-1) == 1
     M = s.shape[0]
     ld_p = ld_p or (nseg * seglen + BK - 1) // BK * BK
@@ -878,6 +878,55 @@ def cross_attention_block(t, kv, pc_q: PackedConv, pc_o: PackedConv, *, batch, n
     if PROFILER.active:
         PROFILER.end()
     return (out, out_ln) if norm_out is not None else out
+
+
+def ff_supported(channels, features):
+    return bool(lib().sdk_ff_supported(channels, features))
+
+
+class PackedFF:
+    """The GEGLU FeedForward's weights packed once for ``feed_forward`` (sdk_ff_pack): proj (Linear(C, 2F):
+    rows [0, F) = a, [F, 2F) = gate) and the output Linear(F, C)."""
+
+    def __init__(self, w1, b1, w2, b2, device):
+        F2, Cc = w1.shape
+        self.channels, self.features = Cc, F2 // 2
+        if not ff_supported(Cc, self.features):
+            raise ValueError(f"sd_amd.PackedFF: unsupported shape channels={Cc} features={self.features}")
+        w1h = w1.detach().to(device=device, dtype=torch.float16).contiguous()
+        w2h = w2.detach().to(device=device, dtype=torch.float16).contiguous()
+        b1f = b1.detach().to(device=device, dtype=torch.float32).contiguous() if b1 is not None else None
+        self.b2 = b2.detach().to(device=device, dtype=torch.float32).contiguous() if b2 is not None else None
+        nbytes = lib().sdk_ff_packed_bytes(Cc, self.features)
+        self.packed = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        check(lib().sdk_ff_pack(_ptr(w1h), _ptr(b1f), _ptr(w2h), _ptr(self.packed), Cc, self.features, _stream()),
+              "ff_pack")
+
+
+def feed_forward(pf: PackedFF, t, residual=None, out=None):
+    """out = residual + Linear2(GEGLU(t)) in one kernel (t, residual: [M, C] fp16 token rows)."""
+    _need_cuda(t, "feed_forward t")
+    M, Cc = t.shape
+    if Cc != pf.channels or t.stride(-1) != 1:
+        raise ValueError("sd_amd.feed_forward: t must be [M, channels] with unit column stride")
+    if out is None:
+        out = torch.empty(M, Cc, dtype=torch.float16, device=t.device)
+    _claim(out)
+    a = FfArgs()
+    a.t, a.out, a.packed = t.data_ptr(), out.data_ptr(), pf.packed.data_ptr()
+    a.b2 = pf.b2.data_ptr() if pf.b2 is not None else None
+    if residual is not None:
+        _need_cuda(residual, "feed_forward residual")
+        a.res, a.res_ld = residual.data_ptr(), residual.stride(0)
+    a.t_ld, a.out_ld = t.stride(0), out.stride(0)
+    a.rows, a.channels, a.features = M, Cc, pf.features
+    if PROFILER.active:
+        PROFILER.begin("feed_forward", None, shape=(M, Cc, pf.features))
+        PROFILER._cur = PROFILER._cur[:2] + (2.0 * M * Cc * 3 * pf.features,) + PROFILER._cur[3:]
+    check(lib().sdk_feed_forward(C.byref(a), _stream()), "feed_forward")
+    if PROFILER.active:
+        PROFILER.end()
+    return out
 
 
 # --------------------------------------------------------------------------- sampler glue
