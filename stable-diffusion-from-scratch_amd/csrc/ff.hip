@@ -85,32 +85,30 @@ __global__ void __launch_bounds__(FF_NT, 1) ff_geglu_kernel(FfParams p) {
   const int m0 = blockIdx.x * FF_ROWS;
   const __amdgpu_buffer_rsrc_t rw = ff_rsrc(p.w, (long long)p.nfb * FF_BLK);
 
-  // this wave's pieces of a stage: byte offset inside the stage's two packed blocks, LDS offset
-  unsigned src[FF_GPW];
-  int dst[FF_GPW];
+  // this wave's pieces of a stage: piece j*8 + wave of the pair's 62 (block = piece / 31); wave-uniform
+  // source / LDS offsets (SGPRs) + the lane's 16 B, selected branch-free (2 VGPRs of addressing)
+  const unsigned lane16 = (unsigned)lane * 16u;
+  const unsigned lane16_b1 = lane < 8 ? lane16 : FF_OOB;   // b1 piece: 128 B, lanes 8.. load zeros
+  unsigned soff[FF_GPW];
+  int doff[FF_GPW];
+  unsigned b1mask = 0;
 #pragma unroll
   for (int j = 0; j < FF_GPW; ++j) {
     const int piece = j * FF_NW + wave;
     const int blk = piece / FF_BPC, q = piece - blk * FF_BPC;
-    if (piece >= FF_PIECES) {                // dummy piece: same count in every wave
-      src[j] = FF_OOB;
-      dst[j] = -1;
-    } else if (q < FF_BPC - 1) {
-      src[j] = (unsigned)(blk * FF_BLK + q * 1024 + lane * 16);
-      dst[j] = blk * FF_BSL + q * 1024;
-    } else {                                 // b1: 128 B, lanes 8.. load zeros
-      src[j] = lane < 8 ? (unsigned)(blk * FF_BLK + FF_W1 + FF_W2 + lane * 16) : FF_OOB;
-      dst[j] = blk * FF_BSL + FF_W1 + FF_W2;
-    }
+    const bool dummy = piece >= FF_PIECES, b1p = !dummy && q == FF_BPC - 1;
+    soff[j] = dummy ? FF_OOB : (unsigned)(blk * FF_BLK + (b1p ? FF_W1 + FF_W2 : q * 1024));
+    doff[j] = dummy ? FF_LDS - 1024 : blk * FF_BSL + (b1p ? FF_W1 + FF_W2 : q * 1024);
+    b1mask |= (b1p ? 1u : 0u) << j;
   }
-  // stage of iteration it (blocks 2 it, 2 it + 1) into ring slot `slot`; past the end: zero pieces
   auto issue = [&](int it, int slot) __attribute__((always_inline)) {
     if constexpr ((DBG & 1) != 0) return;
     const unsigned base = 2 * it < p.nfb ? (unsigned)(2 * it) * FF_BLK : FF_OOB;
 #pragma unroll
     for (int j = 0; j < FF_GPW; ++j) {
-      char* d = dst[j] < 0 ? ffl + FF_LDS - 1024 : ffl + slot * FF_SLOT + dst[j];
-      ff_dma(rw, d, base + src[j]);          // an OOB offset stays past the range
+      const bool dummy = doff[j] == FF_LDS - 1024;
+      char* d = ffl + (dummy ? 0 : slot * FF_SLOT) + doff[j];
+      ff_dma(rw, d, base + soff[j] + (((b1mask >> j) & 1u) ? lane16_b1 : lane16));
     }
   };
 
@@ -154,12 +152,25 @@ __global__ void __launch_bounds__(FF_NT, 1) ff_geglu_kernel(FfParams p) {
         s[12 + q] = q3[q];
       }
     }
+    auto w1frag = [&](int ks) __attribute__((always_inline)) {
+      const int c = 2 * (ks & 3) + hh;
+      return *reinterpret_cast<const h8*>(st + (ks >> 2) * 4096 + fr * 128 + ((c ^ sw) << 4));
+    };
+    constexpr int LA = 4;                    // fragment reads run LA K-steps ahead of their MFMA
+    h8 wa[FF_KS];
+#pragma unroll
+    for (int j = 0; j < LA; ++j) wa[j] = w1frag(j);
 #pragma unroll
     for (int ks = 0; ks < FF_KS; ++ks) {
-      const int c = 2 * (ks & 3) + hh;
-      const h8 a = *reinterpret_cast<const h8*>(st + (ks >> 2) * 4096 + fr * 128 + ((c ^ sw) << 4));
-      if constexpr ((DBG & 2) == 0) s = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, tq[ks], s, 0, 0, 0);
-      else s[ks & 15] += (float)a[0];
+      if (ks + LA < FF_KS) wa[ks + LA] = w1frag(ks + LA);
+      if constexpr ((DBG & 2) == 0) s = __builtin_amdgcn_mfma_f32_32x32x16_f16(wa[ks], tq[ks], s, 0, 0, 0);
+      else s[ks & 15] += (float)wa[ks][0];
+    }
+    __builtin_amdgcn_sched_group_barrier(0x100, LA + 4, 0);
+#pragma unroll
+    for (int i = 0; i < FF_KS; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
     h8 h;
 #pragma unroll

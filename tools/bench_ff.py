@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--fused-only", action="store_true")
     ap.add_argument("--m", type=int, default=None, help="one row count instead of the three shapes")
+    ap.add_argument("--f", type=int, default=1280, help="GEGLU features (SD: 4 x 320)")
     args = ap.parse_args()
     sd_amd_loader.load()
     from sd_amd import ops
@@ -39,7 +40,7 @@ def main():
         ops.AUTOTUNE.load(tab)
     ops.AUTOTUNE.enable(True)
     dev = torch.device("cuda")
-    C, F = 320, 1280
+    C, F = 320, args.f
     g = torch.Generator().manual_seed(0)
     w1 = (torch.randn(2 * F, C, generator=g) / math.sqrt(C)).half()
     b1 = torch.randn(2 * F, generator=g) * 0.2
