@@ -14,7 +14,12 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result"]
 # attention: IEEE mode off + no NaN semantics, so fmaxf on MFMA results is one v_max3 instead of
 # canonicalising v_max x,x copies first (the inputs are finite fp16 products)
-EXTRA = {"attention.hip": ["-mno-amdgpu-ieee", "-fno-honor-nans"]}
+# xattn.hip: no SLP vectorisation (no packed-fp32 v_pk_* math).  With it, the fused norm3 of the
+# <320, 40> block wrote garbage into 4 rows (16 lanes = one VALU pass group) of one 64-row tile in
+# ~0.3 % of launches inside the UNet (never in isolation): a timing-dependent hazard around the
+# packed sums feeding the quad DPP reductions; scalar fp32 code measured 0 / 2,500 differing launches
+# (tools/det_probe4.py, profiles/r3_xattn_determinism.txt)
+EXTRA = {"attention.hip": ["-mno-amdgpu-ieee", "-fno-honor-nans"], "xattn.hip": ["-fno-slp-vectorize"]}
 
 
 def _needs(obj: str, deps) -> bool:

@@ -272,9 +272,10 @@ class _Autotune:
             self.table[key] = (0, 0)
             return self.table[key]
         if a.seg[0].gn_scale or a.seg[0].silu:
-            # a transform prologue: the register-staged kernel, or the halo-tile 3x3 with GroupNorm (+ SiLU)
+            # a transform prologue: the register-staged kernel, the skinny M <= 64 GEMM (SiLU on its A
+            # fragments), or the halo-tile 3x3 with GroupNorm (+ SiLU)
             # applied to its staged input (variants 36 / 37, when a plan exists)
-            cands = (0, 36, 37)
+            cands = (0, 35, 36, 37)
         best, best_t = (0, 0), float("inf")
         info = ConvPlanInfo()
         stream = _stream()

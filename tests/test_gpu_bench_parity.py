@@ -124,6 +124,21 @@ def test_bench_config_short_sample_and_decode_deterministic(bench_c3):
     assert torch.equal(a, b)
 
 
+def test_bench_config_unet_repeat_bitwise(bench_c3):
+    """120 UNet evaluations of the bench batch on one input (graph replay, the committed table): every
+    result bitwise equal to the first.  A rare timing-dependent corruption (4 rows of the fused norm3
+    output in ~0.3 % of <320, 40> cross-attention launches, fixed by building xattn.hip without
+    packed-fp32 code) slipped past the two-run determinism checks; at its old rate 120 evaluations x
+    5 launches catch it with ~85 % probability."""
+    ld, ctx = bench_c3["ld"], bench_c3["ctx"]
+    g = torch.Generator().manual_seed(9)
+    x = (torch.randn(bench_c3["xT"].shape, generator=g) * 3.0).to(DEV)
+    t = torch.full((x.shape[0],), 501, dtype=torch.long, device=DEV)
+    ref = ld.apply_model(x, t, ctx).clone()
+    bad = sum(int(not torch.equal(ld.apply_model(x, t, ctx), ref)) for _ in range(120))
+    assert bad == 0, f"{bad} of 120 evaluations differ from the first"
+
+
 def test_bench_config_decode_b16_batch_chunks_vs_single_images(bench_c3):
     """The bench's B=16 decode runs the 256-channel 512x512 convs as batch chunks (their sources pass
     the 2 GiB buffer range: ops.BUF_LIMIT); images 0 and 15 of it vs the same latents decoded alone
