@@ -18,8 +18,11 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-res
 # <320, 40> block wrote garbage into 4 rows (16 lanes = one VALU pass group) of one 64-row tile in
 # ~0.3 % of launches inside the UNet (never in isolation): a timing-dependent hazard around the
 # packed sums feeding the quad DPP reductions; scalar fp32 code measured 0 / 2,500 differing launches
-# (tools/det_probe4.py, profiles/r3_xattn_determinism.txt)
-EXTRA = {"attention.hip": ["-mno-amdgpu-ieee", "-fno-honor-nans"], "xattn.hip": ["-fno-slp-vectorize"]}
+# (tools/det_probe4.py, profiles/r3_xattn_determinism.txt).  norm.hip the same, so the LayerNorm row math
+# the two share (common.h) compiles to the same scalar code: the fused norms stay bit-identical to
+# sdk_layer_norm.
+EXTRA = {"attention.hip": ["-mno-amdgpu-ieee", "-fno-honor-nans"], "xattn.hip": ["-fno-slp-vectorize"],
+         "norm.hip": ["-fno-slp-vectorize"]}
 
 
 def _needs(obj: str, deps) -> bool:
@@ -41,7 +44,13 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False) -> str
     for src in SOURCES:
         s = os.path.join(CSRC, src)
         o = os.path.join(bdir, src.replace(".hip", ".o"))
-        if force or _needs(o, [s] + headers):
+        flags_file = o + ".flags"
+        fl = " ".join(FLAGS + EXTRA.get(src, []) + (["-DSDK_CONV_DIAGNOSTICS"] if diag else []))
+        stale_flags = not os.path.exists(flags_file) or open(flags_file).read() != fl
+        if stale_flags:
+            with open(flags_file, "w") as f:
+                f.write(fl)
+        if force or stale_flags or _needs(o, [s] + headers):
             dflags = ["-DSDK_CONV_DIAGNOSTICS"] if diag else []
             jobs.append([HIPCC, *FLAGS, *dflags, *EXTRA.get(src, []), "-c", s, "-o", o])
 
