@@ -121,8 +121,10 @@ def test_c3_bench_step_vs_oracle_chain(sdk):
     ref, _ = _oracle_chain(cfg, usd, vsd, xT[0:1].cpu(), ctx[0:1].cpu(), ld.scale_factor)
     print(f"[parity] C3 oracle chain: {time.time() - t0:.0f} s", flush=True)
     # free-running: the GPU's per-step error (~2e-3, teacher-forced above) integrated over 50 steps and
-    # magnified by the chain (amplification above); threshold ~3x the measured 2.05e-2 / 8.5e-2
-    _report("C3 image 0 free-running (50 DDIM steps + decode, B=16 bench step)", img[0:1], ref, 6e-2, 0.25)
+    # magnified by the chain (amplification above): measured 2.36e-3 / 3.67e-3 (profiles/r3_parity_errors.txt;
+    # the 2.05e-2 / 8.5e-2 seen earlier in round 3 came from the fused-norm3 corruption,
+    # profiles/r3_xattn_determinism.txt) -> limits ~3.5x / 5x
+    _report("C3 image 0 free-running (50 DDIM steps + decode, B=16 bench step)", img[0:1], ref, 8e-3, 2e-2)
 
 
 def test_c2_bench_batch_vs_oracle_chain(sdk):
