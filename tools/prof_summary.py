@@ -17,7 +17,8 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CONV = ("conv_glds_kernel", "conv_ph_kernel", "conv_igemm_kernel", "splitk_reduce_kernel", "splitk_reduce_gn_kernel")
+CONV = ("conv_glds_kernel", "conv_ph_kernel", "conv_halo_kernel", "conv_igemm_kernel", "conv_direct_kernel",
+        "conv_skinny_kernel", "splitk_reduce_kernel", "splitk_reduce_gn_kernel")
 
 
 def short(name):
