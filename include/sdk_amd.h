@@ -288,6 +288,23 @@ int sdk_ff_pack(const void* w1, const float* b1, const void* w2, void* packed, i
                 sdk_stream_t stream);
 int sdk_feed_forward(const sdk_ff_args* a, sdk_stream_t stream);
 
+/* ---------------------------------------------------------------- 320-channel token linear
+ * out[m] = [res[m] +] x[m] W^T + b for the 64x64-level transformer blocks' 320 -> 320 projections:
+ * SpatialTransformer.proj_in (openai_model/attention.py:293-300, a 1x1 conv = per-token linear) and the
+ * self-attention's to_out with its residual (:203-206, x = attn1(norm1(x)) + x at :251).  W stays in
+ * registers, the grid walks 32-token blocks (csrc/token.hip).  x / res / out: [rows, ld] fp16, 16-B
+ * aligned, ld % 8 == 0; res may be NULL or alias out; x must not overlap out.  w fp16 [320][320]
+ * (nn.Linear.weight: [out][in]), 16-B aligned; bias fp32 [320] (16-B aligned) or NULL.
+ */
+typedef struct {
+  const void* x; const void* w; const float* bias; const void* res; void* out;
+  int32_t x_ld, res_ld, out_ld;
+  int32_t rows, in_features, out_features;
+} sdk_token_linear_args;
+
+int sdk_token_linear_supported(int32_t in_features, int32_t out_features);
+int sdk_token_linear(const sdk_token_linear_args* a, sdk_stream_t stream);
+
 /* ---------------------------------------------------------------- sampler / glue
  * DDIM update (DDIM/ddim.py:194-204 == ldm/diffusion/ddim.py:197-205), fp32,
  * evaluated op by op without contraction so it is bit-identical to torch's CPU

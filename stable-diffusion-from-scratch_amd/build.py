@@ -9,7 +9,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 BUILD = os.path.join(HERE, "build")
 LIB = os.path.join(HERE, "libsdk_amd.so")
-SOURCES = ["conv.hip", "norm.hip", "attention.hip", "sampler.hip", "xattn.hip", "ff.hip", "probe.hip"]
+SOURCES = ["conv.hip", "norm.hip", "attention.hip", "sampler.hip", "xattn.hip", "ff.hip", "token.hip", "probe.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result"]
 # attention: IEEE mode off + no NaN semantics, so fmaxf on MFMA results is one v_max3 instead of

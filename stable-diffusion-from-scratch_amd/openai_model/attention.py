@@ -92,6 +92,9 @@ XATTN_REASSOC = os.environ.get("SD_AMD_XATTN_REASSOC") != "0"
 # The 320-channel GEGLU FeedForward as one kernel (ops.feed_forward: the 4C intermediate stays in
 # registers); SD_AMD_FUSED_FF=0 keeps the two GEMMs.
 FUSED_FF = os.environ.get("SD_AMD_FUSED_FF") != "0"
+# 320 -> 320 token projections (self-attention to_out + residual, SpatialTransformer proj_in) on the
+# register-resident-weight kernel (csrc/token.hip) with SD_AMD_TOKEN_LINEAR=1 (opt-in until measured)
+TOKEN_LINEAR = os.environ.get("SD_AMD_TOKEN_LINEAR", "0") != "0"
 
 
 class ReassocContext:
@@ -146,6 +149,9 @@ class CrossAttention(nn.Module):
         self._pc_kv = ops.PackedConv([(torch.cat([self.to_k.weight, self.to_v.weight], 0), cd)], None, device=dev)
         self._pc_o = ops.PackedConv([(self.to_out[0].weight, self.heads * self.dim_head)], self.to_out[0].bias,
                                     device=dev)
+        inner = self.heads * self.dim_head
+        self._ptl_o = (ops.PackedTokenLinear(self.to_out[0].weight, self.to_out[0].bias, dev)
+                       if self.self_attn and ops.token_linear_supported(inner, self.to_out[0].out_features) else None)
         if not self.self_attn:
             self._wq32 = self.to_q.weight.detach().to(dev, torch.float32)          # [inner, C]
             self._wo32 = self.to_out[0].weight.detach().to(dev, torch.float32)     # [C, inner]
@@ -203,7 +209,11 @@ class CrossAttention(nn.Module):
             q = ops.linear(self._pc_q, t)
             k, v, nk = kv[:, :inner], kv[:, inner:], Lc
         o = ops.attention(q, k, v, batch=B, heads=self.heads, nq=N, nk=nk, head_dim=self.dim_head, scale=self.scale)
-        out = ops.linear(self._pc_o, o, residual=residual)
+        if TOKEN_LINEAR and self._ptl_o is not None and o.stride(-1) == 1 and \
+                (residual is None or residual.is_contiguous()):
+            out = ops.token_linear(self._ptl_o, o, residual=residual)
+        else:
+            out = ops.linear(self._pc_o, o, residual=residual)
         ops.PROFILER.region = None
         return out
 
@@ -301,6 +311,8 @@ class SpatialTransformer(nn.Module):
     def _prepare(self, dev):
         _gn_prep(self.norm, dev)
         self._pc_in = ops.PackedConv([(self.proj_in.weight, self.in_channels)], self.proj_in.bias, device=dev)
+        self._ptl_in = (ops.PackedTokenLinear(self.proj_in.weight, self.proj_in.bias, dev)
+                        if ops.token_linear_supported(self.in_channels, self.inner_dim) else None)
         self._pc_out = ops.PackedConv([(self.proj_out.weight, self.inner_dim)], self.proj_out.bias, device=dev)
         for blk in self.transformer_blocks:
             blk._prepare(dev)
@@ -313,8 +325,10 @@ class SpatialTransformer(nn.Module):
         # GN materialised by one streaming pass, then the LDS-DMA GEMM (a GN prologue forces the
         # register-staged kernel: 150-190 TF/s on these shapes vs 330-650 for apply + DMA GEMM)
         xn = _gn(self.norm, x)
-        h = ops.conv2d(self._pc_in, xn)
-        tok = h.view(B * H * W, self.inner_dim)
+        if TOKEN_LINEAR and self._ptl_in is not None and xn.is_contiguous():
+            tok = ops.token_linear(self._ptl_in, xn.view(B * H * W, Cc))
+        else:
+            tok = ops.conv2d(self._pc_in, xn).view(B * H * W, self.inner_dim)
         for i, blk in enumerate(self.transformer_blocks):
             tok = blk._run(tok, B, H * W, None if kvs is None else kvs[i], Lc)
         return ops.conv2d(self._pc_out, tok.view(B, H, W, self.inner_dim), residual=x, gn_stats=True)

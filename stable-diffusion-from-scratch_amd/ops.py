@@ -15,7 +15,7 @@ import math
 import torch
 
 from . import _lib
-from ._lib import (ACT_NONE, ACT_QUICK_GELU, AttentionArgs, XAttnArgs, XAttnLnArgs, FfArgs, ConvArgs, ConvPlanInfo, DdimArgs, GroupNormArgs,
+from ._lib import (ACT_NONE, ACT_QUICK_GELU, AttentionArgs, XAttnArgs, XAttnLnArgs, FfArgs, TokenLinearArgs, ConvArgs, ConvPlanInfo, DdimArgs, GroupNormArgs,
                    OUT_GEGLU_F16, OUT_NCHW_F32, OUT_NHWC_F16, OUT_ROWS_F32, check, lib)
 
 BK = 64          # K tile of the conv kernel (packed weight column padding)
@@ -925,6 +925,51 @@ def feed_forward(pf: PackedFF, t, residual=None, out=None):
         PROFILER.begin("feed_forward", None, shape=(M, Cc, pf.features))
         PROFILER._cur = PROFILER._cur[:2] + (2.0 * M * Cc * 3 * pf.features,) + PROFILER._cur[3:]
     check(lib().sdk_feed_forward(C.byref(a), _stream()), "feed_forward")
+    if PROFILER.active:
+        PROFILER.end()
+    return out
+
+
+def token_linear_supported(in_features, out_features):
+    return bool(lib().sdk_token_linear_supported(in_features, out_features))
+
+
+class PackedTokenLinear:
+    """A 320 -> 320 Linear / 1x1 conv for ``token_linear`` (sdk_token_linear): fp16 [out][in] weight
+    (nn.Linear layout; a [out, in, 1, 1] conv weight is flattened), fp32 bias."""
+
+    def __init__(self, w, b, device):
+        w = w.detach().reshape(w.shape[0], -1)
+        if not token_linear_supported(w.shape[1], w.shape[0]):
+            raise ValueError(f"sd_amd.PackedTokenLinear: unsupported shape {tuple(w.shape)}")
+        self.features = w.shape[0]
+        self.w = w.to(device=device, dtype=torch.float16).contiguous()
+        self.b = b.detach().to(device=device, dtype=torch.float32).contiguous() if b is not None else None
+
+
+def token_linear(pk: PackedTokenLinear, x, residual=None, out=None):
+    """out = [residual +] x W^T + b (x, residual: [M, 320] fp16 token rows; out may be residual)."""
+    _need_cuda(x, "token_linear x")
+    M, K = x.shape
+    if K != pk.features or x.stride(-1) != 1:
+        raise ValueError("sd_amd.token_linear: x must be [M, 320] with unit column stride")
+    if out is None:
+        out = torch.empty(M, pk.features, dtype=torch.float16, device=x.device)
+    _claim(out)
+    a = TokenLinearArgs()
+    a.x, a.w, a.out = x.data_ptr(), pk.w.data_ptr(), out.data_ptr()
+    a.bias = pk.b.data_ptr() if pk.b is not None else None
+    if residual is not None:
+        _need_cuda(residual, "token_linear residual")
+        if residual.shape != (M, pk.features) or residual.stride(-1) != 1:
+            raise ValueError("sd_amd.token_linear: residual must be [M, 320] with unit column stride")
+        a.res, a.res_ld = residual.data_ptr(), residual.stride(0)
+    a.x_ld, a.out_ld = x.stride(0), out.stride(0)
+    a.rows, a.in_features, a.out_features = M, K, pk.features
+    if PROFILER.active:
+        PROFILER.begin("token_linear", None, shape=(M, pk.features, K))
+        PROFILER._cur = PROFILER._cur[:2] + (2.0 * M * K * pk.features,) + PROFILER._cur[3:]
+    check(lib().sdk_token_linear(C.byref(a), _stream()), "token_linear")
     if PROFILER.active:
         PROFILER.end()
     return out
