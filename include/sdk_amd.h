@@ -305,6 +305,13 @@ typedef struct {
 int sdk_token_linear_supported(int32_t in_features, int32_t out_features);
 int sdk_token_linear(const sdk_token_linear_args* a, sdk_stream_t stream);
 
+/* The same projection, also writing out_ln[m] = LayerNorm(out[m]) (fp32 gamma / beta [320], 16-B aligned;
+ * the same bits as sdk_layer_norm on out): SpatialTransformer.proj_in followed by the first
+ * BasicTransformerBlock's norm1 (openai_model/attention.py:330 then :251, x = attn1(norm1(x)) + x), one
+ * launch instead of two.  out_ln [rows, out_ln_ld] must not overlap x, res or out. */
+int sdk_token_linear_ln(const sdk_token_linear_args* a, const float* gamma, const float* beta, float eps,
+                        void* out_ln, int32_t out_ln_ld, sdk_stream_t stream);
+
 /* ---------------------------------------------------------------- sampler / glue
  * DDIM update (DDIM/ddim.py:194-204 == ldm/diffusion/ddim.py:197-205), fp32,
  * evaluated op by op without contraction so it is bit-identical to torch's CPU

@@ -59,23 +59,37 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
 }
 
-// Cross-lane moves without the LDS crossbar (ds_bpermute is what __shfl lowers to: one LDS round
-// trip per step, and a 6-step butterfly per row serialised the fused norms of xattn.hip at 10 us).
+// Cross-lane moves inside groups of 4 / 16 lanes.  SDK_XLANE_DPP (diagnostics only) selects the DPP
+// form (v_mov_b32_dpp quad_perm / row_ror); the default is ds_swizzle_b32 (quad-perm and xor bit
+// modes: a lane crossbar op of the LDS pipe, no LDS memory, counted by lgkmcnt like any LDS access).
+// Round 3 traced a rare corruption of the fused norm3 output (one 16-lane group's LayerNorm variance
+// <= 0) to the DPP reductions of ln_quad_stats in an SLP-vectorised build; DESIGN.md §4 has the record.
+#ifndef SDK_XLANE_DPP
+#define SDK_XLANE_DPP 0
+#endif
+// CTRL: a DPP quad_perm code (0x00-0xFF: four 2-bit source lanes) or 0x124 / 0x128 (row_ror:4 / 8 in
+// the DPP form, xor 4 / xor 8 inside 32-lane halves in the swizzle form: the same set of summands)
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float x) {
+  static_assert(CTRL <= 0xFF || CTRL == 0x124 || CTRL == 0x128, "dpp_f: quad_perm, row_ror:4 or row_ror:8");
+#if SDK_XLANE_DPP
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+#else
+  constexpr int pat = CTRL <= 0xFF ? 0x8000 | CTRL : (0x1F | ((CTRL == 0x124 ? 4 : 8) << 10));
+  return __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, x), pat));
+#endif
 }
 __device__ __forceinline__ float readlane_f(float x, int l) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
 }
-// Sum over the 64 lanes, the same bits in every lane: quad butterfly (DPP quad_perm), 16-lane rows
-// by two rotations (DPP row_ror), the four row sums read out of lanes 0 / 16 / 32 / 48 and added in
-// a fixed order (a wave-uniform value).
+// Sum over the 64 lanes, the same bits in every lane: quad butterfly, then the 16-lane group by two
+// more steps, the four group sums read out of lanes 0 / 16 / 32 / 48 and added in a fixed order (a
+// wave-uniform value).
 __device__ __forceinline__ float wave_sum_f(float x) {
   x += dpp_f<0xB1>(x);    // quad_perm [1,0,3,2]
   x += dpp_f<0x4E>(x);    // quad_perm [2,3,0,1]
-  x += dpp_f<0x124>(x);   // row_ror:4
-  x += dpp_f<0x128>(x);   // row_ror:8
+  x += dpp_f<0x124>(x);
+  x += dpp_f<0x128>(x);
   return (readlane_f(x, 0) + readlane_f(x, 16)) + (readlane_f(x, 32) + readlane_f(x, 48));
 }
 
@@ -85,8 +99,13 @@ __device__ __forceinline__ float wave_sum_f(float x) {
 // come out of ONE pair of wave sums: of (x - x0) and (x - x0)^2 around a pivot x0 taken from the
 // row itself (its first element), so the E[d^2] - E[d]^2 form does not cancel.  Branch-free, so
 // independent rows interleave.
+// The row math below fixes every rounding point (contraction off, the fused steps written as fmaf):
+// the same source then compiles to the same bits whether or not the translation unit is built with SLP
+// vectorisation (packed v_pk_*_f32 code) — the separate LayerNorm launch (norm.hip) and the norms fused
+// into the cross-attention block (xattn.hip) and the token linear (token.hip) agree bit for bit.
 template <int MAXV>
 __device__ __forceinline__ void ln_row_stats(const h8 (&v)[MAXV], int cols, float eps, float& mean, float& rstd) {
+#pragma clang fp contract(off)
   const int lane = threadIdx.x & 63;
   const int c8 = cols / 8;
   const float x0 = readlane_f((float)v[0][0], 0);
@@ -98,26 +117,27 @@ __device__ __forceinline__ void ln_row_stats(const h8 (&v)[MAXV], int cols, floa
     for (int j = 0; j < 8; ++j) {
       const float d = ok ? (float)v[i][j] - x0 : 0.f;
       s1 += d;
-      s2 += d * d;
+      s2 = __builtin_fmaf(d, d, s2);
     }
   }
   s1 = wave_sum_f(s1);
   s2 = wave_sum_f(s2);
   const float inv_n = 1.f / cols;
   const float dm = s1 * inv_n;
-  const float var = fmaxf(s2 * inv_n - dm * dm, 0.f);
+  const float var = fmaxf(__builtin_fmaf(-dm, dm, s2 * inv_n), 0.f);
   mean = x0 + dm;
   rstd = rsqrtf(var + eps);
 }
 
 // LayerNorm of rows of C = 32 * CPL channels (C <= 640 on the SD path), FOUR lanes per row (16 rows
 // per wave): lane q = lane & 3 of a row holds its 8-channel chunks k = q + 4 i (i < CPL), so a row's
-// sums are in-lane except for one quad butterfly (DPP quad_perm: the same bits in all four lanes),
-// and a wave normalises 16 rows with the instructions a wave-per-row layout spends on ~3.  Shared
-// by layer_norm_quad_kernel (norm.hip) and the cross-attention block's fused norm2 / norm3
-// (xattn.hip), so both produce the same bits.  Pivot x0 = the row's first element (lane q = 0).
+// sums are in-lane except for one quad butterfly (the same bits in all four lanes), and a wave
+// normalises 16 rows with the instructions a wave-per-row layout spends on ~3.  Shared by
+// layer_norm_quad_kernel (norm.hip), the cross-attention block's fused norm2 / norm3 (xattn.hip) and
+// token_linear_ln (token.hip), so all produce the same bits.  Pivot x0 = the row's first element.
 template <int CPL>
 __device__ __forceinline__ void ln_quad_stats(const h8 (&v)[CPL], float eps, float& mean, float& rstd) {
+#pragma clang fp contract(off)
   const float x0 = dpp_f<0x00>((float)v[0][0]);    // quad_perm [0,0,0,0]
   float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -126,7 +146,7 @@ __device__ __forceinline__ void ln_quad_stats(const h8 (&v)[CPL], float eps, flo
     for (int j = 0; j < 8; ++j) {
       const float d = (float)v[i][j] - x0;
       s1 += d;
-      s2 += d * d;
+      s2 = __builtin_fmaf(d, d, s2);
     }
   s1 += dpp_f<0xB1>(s1);
   s2 += dpp_f<0xB1>(s2);
@@ -134,28 +154,30 @@ __device__ __forceinline__ void ln_quad_stats(const h8 (&v)[CPL], float eps, flo
   s2 += dpp_f<0x4E>(s2);
   const float inv_n = 1.f / (32 * CPL);
   const float dm = s1 * inv_n;
-  const float var = fmaxf(s2 * inv_n - dm * dm, 0.f);
+  const float var = fmaxf(__builtin_fmaf(-dm, dm, s2 * inv_n), 0.f);
   mean = x0 + dm;
   rstd = rsqrtf(var + eps);
 }
 
 // normalised chunk k of a row: gamma / beta (fp32) from LDS (`gb`: gamma[C] then beta[C])
 __device__ __forceinline__ h8 ln_quad_apply(const h8& v, float mean, float rstd, const float* gb, int C, int k) {
+#pragma clang fp contract(off)
   const f4 g0 = *reinterpret_cast<const f4*>(gb + 8 * k), g1 = *reinterpret_cast<const f4*>(gb + 8 * k + 4);
   const f4 b0 = *reinterpret_cast<const f4*>(gb + C + 8 * k), b1 = *reinterpret_cast<const f4*>(gb + C + 8 * k + 4);
   h8 o;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    o[j] = (half_t)(((float)v[j] - mean) * rstd * g0[j] + b0[j]);
-    o[4 + j] = (half_t)(((float)v[4 + j] - mean) * rstd * g1[j] + b1[j]);
+    o[j] = (half_t)__builtin_fmaf(((float)v[j] - mean) * rstd, g0[j], b0[j]);
+    o[4 + j] = (half_t)__builtin_fmaf(((float)v[4 + j] - mean) * rstd, g1[j], b1[j]);
   }
   return o;
 }
 
 __device__ __forceinline__ h8 ln_apply8(const h8& v, float mean, float rstd, const float (&g)[8], const float (&b)[8]) {
+#pragma clang fp contract(off)
   h8 o;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) o[j] = (half_t)(((float)v[j] - mean) * rstd * g[j] + b[j]);
+  for (int j = 0; j < 8; ++j) o[j] = (half_t)__builtin_fmaf(((float)v[j] - mean) * rstd, g[j], b[j]);
   return o;
 }
 

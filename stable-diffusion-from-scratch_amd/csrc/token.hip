@@ -17,6 +17,11 @@
 //  * The fp32 accumulators + bias are rounded to fp16 into a second LDS tile, then every thread stores
 //    whole 16-B row chunks (+ the residual, loaded before the MFMAs) — the conv epilogue's rounding
 //    points (acc + b -> fp16, then + res -> fp16).
+//  * LN = true (sdk_token_linear_ln): the finished rows go back into that tile and two waves apply a
+//    LayerNorm to them with the row math of layer_norm_quad_kernel (common.h ln_quad_stats /
+//    ln_quad_apply: the same bits), written as a second output — the SpatialTransformer's proj_in
+//    emits the first block's norm1 input AND output, so the 64x64 level has no LayerNorm launch
+//    (attention.py:251: x = attn1(norm1(x)) + x right after proj_in at :330).
 #include "common.h"
 
 namespace sdk {
@@ -32,13 +37,27 @@ constexpr int TL_CPT = TL_ROWS * TL_CPR / 256;   // chunks per thread per block 
 constexpr int TL_TG = TL_ROWS / 16;     // 16-token groups per block
 static_assert(TL_ROWS * TL_CPR % 256 == 0, "whole chunks per thread");
 
+struct TokenLn {
+  const float* gamma; const float* beta; float eps;
+  half_t* out; int out_ld;
+};
+
+template <bool LN>
 __global__ void __launch_bounds__(256, 1) token_linear320_kernel(const half_t* __restrict__ x, int x_ld,
                                                                  const half_t* __restrict__ w,
                                                                  const float* __restrict__ bias, const half_t* res,
-                                                                 int res_ld, half_t* out, int out_ld, int rows) {
+                                                                 int res_ld, half_t* out, int out_ld, int rows,
+                                                                 TokenLn ln) {
   __shared__ __attribute__((aligned(16))) half_t xs[TL_ROWS * TL_LD];
   __shared__ __attribute__((aligned(16))) half_t os[TL_ROWS * TL_LD];
+  __shared__ __attribute__((aligned(16))) float gb[LN ? 2 * TLC : 4];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  if constexpr (LN) {   // gamma | beta for ln_quad_apply; the first block's barrier orders these writes
+    if (t < TLC / 4) {
+      *reinterpret_cast<f4*>(gb + 4 * t) = *reinterpret_cast<const f4*>(ln.gamma + 4 * t);
+      *reinterpret_cast<f4*>(gb + TLC + 4 * t) = *reinterpret_cast<const f4*>(ln.beta + 4 * t);
+    }
+  }
   const int r16 = lane & 15, kq = lane >> 4;
   const int nblk = (rows + TL_ROWS - 1) / TL_ROWS;
   int b = blockIdx.x;
@@ -124,20 +143,42 @@ __global__ void __launch_bounds__(256, 1) token_linear320_kernel(const half_t* _
         for (int j = 0; j < 8; ++j) v[j] = (half_t)((float)v[j] + (float)rr[i][j]);
       }
       *reinterpret_cast<h8*>(out + (size_t)row * out_ld + ccol[i]) = v;
+      if constexpr (LN) *reinterpret_cast<h8*>(os + crow[i] * TL_LD + ccol[i]) = v;
+    }
+    if constexpr (LN) {
+      // waves 0 / 1: rows [16 wave, 16 wave + 16) of the block, four lanes per row (lane q holds chunks
+      // q + 4 i); the next block's os writes come after its first barrier, so this tile stays intact
+      __syncthreads();
+      if (wave < TL_ROWS / 16) {
+        constexpr int CPL = TLC / 32;
+        const int q = lane & 3, r = 16 * wave + (lane >> 2), row = b * TL_ROWS + r;
+        h8 v[CPL];
+#pragma unroll
+        for (int i = 0; i < CPL; ++i) v[i] = *reinterpret_cast<const h8*>(os + r * TL_LD + 8 * (q + 4 * i));
+        float mean, rstd;
+        ln_quad_stats<CPL>(v, ln.eps, mean, rstd);
+        if (row < rows) {
+          half_t* yr = ln.out + (size_t)row * ln.out_ld + 8 * q;
+#pragma unroll
+          for (int i = 0; i < CPL; ++i)
+            *reinterpret_cast<h8*>(yr + 32 * i) = ln_quad_apply(v[i], mean, rstd, gb, TLC, q + 4 * i);
+        }
+      }
     }
   }
 }
 
-}  // namespace
-}  // namespace sdk
-
-using namespace sdk;
-
-extern "C" int sdk_token_linear_supported(int32_t in_features, int32_t out_features) {
-  return in_features == TLC && out_features == TLC ? 1 : 0;
+template <bool LN>
+int token_linear_launch(const sdk_token_linear_args* a, const TokenLn& ln, hipStream_t s) {
+  const int nblk = (a->rows + TL_ROWS - 1) / TL_ROWS;
+  const unsigned grid = (unsigned)(nblk < 256 ? nblk : 256);
+  hipLaunchKernelGGL(token_linear320_kernel<LN>, dim3(grid), dim3(256), 0, s, (const half_t*)a->x, a->x_ld,
+                     (const half_t*)a->w, a->bias, (const half_t*)a->res, a->res_ld, (half_t*)a->out, a->out_ld,
+                     a->rows, ln);
+  return check_launch(LN ? "token_linear_ln" : "token_linear");
 }
 
-extern "C" int sdk_token_linear(const sdk_token_linear_args* a, sdk_stream_t stream) {
+int token_linear_check(const sdk_token_linear_args* a) {
   if (!a || !a->x || !a->w || !a->out) return fail(SDK_EINVAL, "token_linear: null pointer");
   if (a->in_features != TLC || a->out_features != TLC)
     return fail(SDK_EINVAL, "token_linear: in_features and out_features must be 320");
@@ -151,10 +192,35 @@ extern "C" int sdk_token_linear(const sdk_token_linear_args* a, sdk_stream_t str
   const char *x0 = (const char*)a->x, *o0 = (const char*)a->out;
   const long long xb = ((long long)(a->rows - 1) * a->x_ld + TLC) * 2, ob = ((long long)(a->rows - 1) * a->out_ld + TLC) * 2;
   if (x0 < o0 + ob && o0 < x0 + xb) return fail(SDK_EINVAL, "token_linear: x and out overlap");
-  const int nblk = (a->rows + TL_ROWS - 1) / TL_ROWS;
-  const unsigned grid = (unsigned)(nblk < 256 ? nblk : 256);
-  hipLaunchKernelGGL(token_linear320_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const half_t*)a->x,
-                     a->x_ld, (const half_t*)a->w, a->bias, (const half_t*)a->res, a->res_ld, (half_t*)a->out,
-                     a->out_ld, a->rows);
-  return check_launch("token_linear");
+  return SDK_OK;
+}
+
+}  // namespace
+}  // namespace sdk
+
+using namespace sdk;
+
+extern "C" int sdk_token_linear_supported(int32_t in_features, int32_t out_features) {
+  return in_features == TLC && out_features == TLC ? 1 : 0;
+}
+
+extern "C" int sdk_token_linear(const sdk_token_linear_args* a, sdk_stream_t stream) {
+  if (int e = token_linear_check(a)) return e;
+  return token_linear_launch<false>(a, TokenLn{}, (hipStream_t)stream);
+}
+
+extern "C" int sdk_token_linear_ln(const sdk_token_linear_args* a, const float* gamma, const float* beta, float eps,
+                                   void* out_ln, int32_t out_ln_ld, sdk_stream_t stream) {
+  if (int e = token_linear_check(a)) return e;
+  if (!gamma || !beta || !out_ln) return fail(SDK_EINVAL, "token_linear_ln: null gamma / beta / out_ln");
+  if (((uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)out_ln) & 15 || out_ln_ld % 8 || out_ln_ld < TLC)
+    return fail(SDK_EINVAL, "token_linear_ln: gamma / beta / out_ln must be 16-B aligned, out_ln_ld % 8 == 0 and >= 320");
+  // out_ln is written by the LN waves while other workgroups still read x / res / write out
+  const char *x0 = (const char*)a->x, *l0 = (const char*)out_ln, *o0 = (const char*)a->out;
+  const long long lb = ((long long)(a->rows - 1) * out_ln_ld + TLC) * 2;
+  const long long xb = ((long long)(a->rows - 1) * a->x_ld + TLC) * 2, ob = ((long long)(a->rows - 1) * a->out_ld + TLC) * 2;
+  if ((x0 < l0 + lb && l0 < x0 + xb) || (o0 < l0 + lb && l0 < o0 + ob) ||
+      (a->res && (const char*)a->res < l0 + lb && l0 < (const char*)a->res + ((long long)(a->rows - 1) * a->res_ld + TLC) * 2))
+    return fail(SDK_EINVAL, "token_linear_ln: out_ln overlaps x, res or out");
+  return token_linear_launch<true>(a, TokenLn{gamma, beta, eps, (half_t*)out_ln, out_ln_ld}, (hipStream_t)stream);
 }

@@ -92,9 +92,11 @@ XATTN_REASSOC = os.environ.get("SD_AMD_XATTN_REASSOC") != "0"
 # The 320-channel GEGLU FeedForward as one kernel (ops.feed_forward: the 4C intermediate stays in
 # registers); SD_AMD_FUSED_FF=0 keeps the two GEMMs.
 FUSED_FF = os.environ.get("SD_AMD_FUSED_FF") != "0"
-# 320 -> 320 token projections (self-attention to_out + residual, SpatialTransformer proj_in) on the
-# register-resident-weight kernel (csrc/token.hip) with SD_AMD_TOKEN_LINEAR=1 (opt-in until measured)
-TOKEN_LINEAR = os.environ.get("SD_AMD_TOKEN_LINEAR", "0") != "0"
+# 320 -> 320 token projections (self-attention to_out + residual, SpatialTransformer proj_in with the
+# first block's norm1 emitted from the same tile) on the register-resident-weight kernel (csrc/token.hip);
+# same-box A/B: UNet step 19.58 -> 19.44 ms (profiles/r4_token_linear_ab.txt).  SD_AMD_TOKEN_LINEAR=0
+# keeps the tiled GEMM + separate LayerNorm
+TOKEN_LINEAR = os.environ.get("SD_AMD_TOKEN_LINEAR", "1") != "0"
 
 
 class ReassocContext:
@@ -273,8 +275,10 @@ class BasicTransformerBlock(nn.Module):
         for n in (self.norm1, self.norm2, self.norm3):
             _ln_prep(n, dev)
 
-    def _run(self, tok, B, N, kv=None, Lc=None):
-        t = ops.layer_norm(tok, self.norm1._g, self.norm1._b, self.norm1.eps)
+    def _run(self, tok, B, N, kv=None, Lc=None, t=None):
+        """``t``: norm1(tok) when the producer of ``tok`` emitted it (token_linear with a norm)."""
+        if t is None:
+            t = ops.layer_norm(tok, self.norm1._g, self.norm1._b, self.norm1.eps)
         tok = self.attn1._run(t, tok, B, N)
         a2 = self.attn2
         if (kv is not None and FUSED_XATTN_NORMS and tok.stride(-1) == 1
@@ -325,12 +329,18 @@ class SpatialTransformer(nn.Module):
         # GN materialised by one streaming pass, then the LDS-DMA GEMM (a GN prologue forces the
         # register-staged kernel: 150-190 TF/s on these shapes vs 330-650 for apply + DMA GEMM)
         xn = _gn(self.norm, x)
+        t1 = None
         if TOKEN_LINEAR and self._ptl_in is not None and xn.is_contiguous():
-            tok = ops.token_linear(self._ptl_in, xn.view(B * H * W, Cc))
+            # proj_in + the first block's norm1 in one launch (the LayerNorm rows from the same tile)
+            n1 = self.transformer_blocks[0].norm1 if len(self.transformer_blocks) else None
+            if n1 is not None:
+                tok, t1 = ops.token_linear(self._ptl_in, xn.view(B * H * W, Cc), norm=(n1._g, n1._b, n1.eps))
+            else:
+                tok = ops.token_linear(self._ptl_in, xn.view(B * H * W, Cc))
         else:
             tok = ops.conv2d(self._pc_in, xn).view(B * H * W, self.inner_dim)
         for i, blk in enumerate(self.transformer_blocks):
-            tok = blk._run(tok, B, H * W, None if kvs is None else kvs[i], Lc)
+            tok = blk._run(tok, B, H * W, None if kvs is None else kvs[i], Lc, t=t1 if i == 0 else None)
         return ops.conv2d(self._pc_out, tok.view(B, H, W, self.inner_dim), residual=x, gn_stats=True)
 
 

@@ -652,8 +652,9 @@ def group_norm_scale_shift(x, gamma, beta, eps, groups=32):
     return scale, shift
 
 
-# ResBlock 3x3 convs apply GroupNorm + SiLU to their own staged input (no normalised tensor written) where
-# the halo-tile kernel has a plan; SD_AMD_FUSED_GN_CONV=0 keeps the materialised zero-bordered GN output
+# Opt-in (SD_AMD_FUSED_GN_CONV=1; off by default): ResBlock 3x3 convs apply GroupNorm + SiLU to their own
+# staged input (no normalised tensor written) where the halo-tile kernel has a plan.  Off because the
+# same-box A/B lost: GroupNorm -25 ms but convs +99 ms per sample (profiles/r3_gn_fused_conv_ab.txt)
 FUSED_GN_CONV = __import__("os").environ.get("SD_AMD_FUSED_GN_CONV", "0") == "1"
 _FUSABLE = {}
 
@@ -947,8 +948,10 @@ class PackedTokenLinear:
         self.b = b.detach().to(device=device, dtype=torch.float32).contiguous() if b is not None else None
 
 
-def token_linear(pk: PackedTokenLinear, x, residual=None, out=None):
-    """out = [residual +] x W^T + b (x, residual: [M, 320] fp16 token rows; out may be residual)."""
+def token_linear(pk: PackedTokenLinear, x, residual=None, out=None, norm=None):
+    """out = [residual +] x W^T + b (x, residual: [M, 320] fp16 token rows; out may be residual).
+    ``norm=(gamma, beta, eps)`` (fp32 [320]) also returns LayerNorm(out) (sdk_token_linear_ln, the same
+    bits as ``layer_norm(out, ...)``): ``(out, out_ln)``."""
     _need_cuda(x, "token_linear x")
     M, K = x.shape
     if K != pk.features or x.stride(-1) != 1:
@@ -969,10 +972,20 @@ def token_linear(pk: PackedTokenLinear, x, residual=None, out=None):
     if PROFILER.active:
         PROFILER.begin("token_linear", None, shape=(M, pk.features, K))
         PROFILER._cur = PROFILER._cur[:2] + (2.0 * M * K * pk.features,) + PROFILER._cur[3:]
-    check(lib().sdk_token_linear(C.byref(a), _stream()), "token_linear")
+    if norm is None:
+        check(lib().sdk_token_linear(C.byref(a), _stream()), "token_linear")
+    else:
+        g, bt, eps = norm
+        _need_cuda(g, "token_linear_ln gamma", torch.float32)
+        _need_cuda(bt, "token_linear_ln beta", torch.float32)
+        if g.numel() != pk.features or bt.numel() != pk.features:
+            raise ValueError("sd_amd.token_linear: norm gamma / beta must have 320 elements")
+        out_ln = torch.empty(M, pk.features, dtype=torch.float16, device=x.device)
+        check(lib().sdk_token_linear_ln(C.byref(a), g.data_ptr(), bt.data_ptr(), float(eps), out_ln.data_ptr(),
+                                        out_ln.stride(0), _stream()), "token_linear_ln")
     if PROFILER.active:
         PROFILER.end()
-    return out
+    return out if norm is None else (out, out_ln)
 
 
 # --------------------------------------------------------------------------- sampler glue

@@ -88,3 +88,45 @@ def test_token_linear_rejects(ops, sdk):
     assert _lib.lib().sdk_token_linear(a, None) != 0          # x overlaps out
     a.in_features = a.out_features = 640
     assert _lib.lib().sdk_token_linear(a, None) != 0
+
+
+@pytest.mark.parametrize("M,with_res", [(65536, False), (1000, True), (7, False)])
+def test_token_linear_ln_matches_layer_norm(ops, M, with_res):
+    """sdk_token_linear_ln: proj_in + norm1 in one launch.  out is bitwise the plain token linear's, out_ln
+    bitwise sdk_layer_norm of that out (the shared quad row math), and both within fp tolerance of fp32."""
+    w, b, x, res = _case(M, 11 + M)
+    dev = torch.device(DEV)
+    g = torch.Generator().manual_seed(M)
+    gamma = (1 + 0.1 * torch.randn(320, generator=g)).to(DEV)
+    beta = (0.1 * torch.randn(320, generator=g)).to(DEV)
+    pk = ops.PackedTokenLinear(w, b, dev)
+    xd, rd = x.to(DEV), (res.to(DEV) if with_res else None)
+    plain = ops.token_linear(pk, xd, residual=rd)
+    out, out_ln = ops.token_linear(pk, xd, residual=rd, norm=(gamma, beta, 1e-5))
+    assert torch.equal(out, plain)
+    sep = ops.layer_norm(plain, gamma, beta, 1e-5)
+    d = (out_ln.float() - sep.float()).abs().max().item()
+    print(f"[token_linear_ln] M={M}: max |diff| vs layer_norm {d:.3e}", flush=True)
+    assert torch.equal(out_ln, sep)
+    ref = torch.nn.functional.layer_norm(plain.float(), (320,), gamma.float(), beta.float(), 1e-5)
+    assert rel_l2(out_ln, ref.cpu()) < 2e-3
+    # repeated launches are bitwise stable
+    for _ in range(3):
+        o2, l2 = ops.token_linear(pk, xd, residual=rd, norm=(gamma, beta, 1e-5))
+        assert torch.equal(o2, out) and torch.equal(l2, out_ln)
+
+
+def test_token_linear_ln_rejects_overlap(ops, sdk):
+    from sd_amd import _lib
+    x = torch.zeros(64, 320, dtype=torch.float16, device=DEV)
+    o = torch.zeros(64, 320, dtype=torch.float16, device=DEV)
+    gb = torch.ones(320, dtype=torch.float32, device=DEV)
+    w = torch.zeros(320, 320, dtype=torch.float16, device=DEV)
+    a = _lib.TokenLinearArgs()
+    a.x, a.w, a.out = x.data_ptr(), w.data_ptr(), o.data_ptr()
+    a.x_ld = a.out_ld = 320
+    a.rows, a.in_features, a.out_features = 64, 320, 320
+    L = _lib.lib()
+    assert L.sdk_token_linear_ln(a, gb.data_ptr(), gb.data_ptr(), 1e-5, o.data_ptr(), 320, None) != 0   # out_ln == out
+    assert L.sdk_token_linear_ln(a, gb.data_ptr(), gb.data_ptr(), 1e-5, x.data_ptr(), 320, None) != 0   # out_ln == x
+    assert L.sdk_token_linear_ln(a, None, gb.data_ptr(), 1e-5, w.data_ptr(), 320, None) != 0
