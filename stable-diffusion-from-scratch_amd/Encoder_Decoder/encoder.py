@@ -89,7 +89,7 @@ class Encoder(nn.Module):
 
     def _run(self, x_nhwc):
         """x_nhwc: fp16 [B, H, W, in_pad] → fp32 NCHW conv_out (∘ quant_conv) output."""
-        h = ops.conv2d(self._pc_in, x_nhwc)
+        h = ops.conv2d(self._pc_in, x_nhwc, gn_stats=True)     # feeds down[0].block[0].norm1
         for i_level in range(self.num_resolutions):
             down = self.down[i_level]
             for i_block in range(self.num_res_blocks):
@@ -174,7 +174,7 @@ class Decoder(nn.Module):
 
     def _run(self, z_nhwc):
         """z_nhwc: fp16 [B, h, w, zc_pad] → fp32 NCHW image."""
-        h = ops.conv2d(self._pc_in, z_nhwc)
+        h = ops.conv2d(self._pc_in, z_nhwc, gn_stats=True)     # feeds mid.block_1.norm1
         h = self.mid.block_1._run(h)
         h = self.mid.attn_1._run(h)
         h = self.mid.block_2._run(h)

@@ -40,7 +40,7 @@ class FlashAttentionBlock(nn.Module):
         qkv = ops.conv2d(self._pc_qkv, xn).view(B * H * W, 3 * C)
         o = ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], batch=B, heads=self.num_heads, nq=H * W,
                           nk=H * W, head_dim=self.head_dim, scale=self.head_dim ** -0.5)
-        return ops.conv2d(self._pc_o, o.view(B, H, W, C), residual=x)
+        return ops.conv2d(self._pc_o, o.view(B, H, W, C), residual=x, gn_stats=True)   # feeds a GroupNorm
 
 
 def make_attention(in_channels, attention_type="vanilla"):

@@ -46,7 +46,8 @@ class Upsample(nn.Module):
         self._pc = ops.PackedConv([(self.conv.weight, self.in_channels)], self.conv.bias, device=dev)
 
     def _run(self, x):
-        return ops.conv2d(self._pc, x, upsample=True)
+        # the output feeds the next ResnetBlock's norm1: the conv emits its GroupNorm statistics
+        return ops.conv2d(self._pc, x, upsample=True, gn_stats=True)
 
 
 class Downsample(nn.Module):
@@ -67,7 +68,7 @@ class Downsample(nn.Module):
         self._pc = ops.PackedConv([(self.conv.weight, self.in_channels)], self.conv.bias, device=dev)
 
     def _run(self, x):
-        return ops.conv2d(self._pc, x, stride=2, pad=0, pad_end=1)
+        return ops.conv2d(self._pc, x, stride=2, pad=0, pad_end=1, gn_stats=True)
 
 
 class ResnetBlock(nn.Module):
@@ -110,12 +111,14 @@ class ResnetBlock(nn.Module):
     def _run(self, x, temb=None):
         if temb is not None:
             raise NotImplementedError("sd_amd: the VAE ResnetBlock path has no timestep embedding")
-        # zero-bordered GN+SiLU outputs: both 3x3 convs run with pad 0 (mask-free gather)
+        # zero-bordered GN+SiLU outputs: both 3x3 convs run with pad 0 (mask-free gather); both outputs
+        # feed a GroupNorm (norm2 / the next block's norm1, an attention norm or norm_out), so the convs
+        # emit its statistics from their epilogues (no statistics pass over the tensor)
         gp, cp = ops.gn_conv_pad()
-        h = ops.conv2d(self._pc1, gn_act(self.norm1, x, silu=True, pad=gp), pad=cp)
+        h = ops.conv2d(self._pc1, gn_act(self.norm1, x, silu=True, pad=gp), pad=cp, gn_stats=True)
         ha = gn_act(self.norm2, h, silu=True, pad=gp)
         if self._mode == "identity":
-            return ops.conv2d(self._pc2, ha, pad=cp, residual=x)
+            return ops.conv2d(self._pc2, ha, pad=cp, residual=x, gn_stats=True)
         if self._mode == "fused":
-            return ops.conv2d(self._pc2, ha, pad=cp, seg2=(x, None, False))
-        return ops.conv2d(self._pc2, ha, pad=cp, residual=ops.conv2d(self._pcs, x))
+            return ops.conv2d(self._pc2, ha, pad=cp, seg2=(x, None, False), gn_stats=True)
+        return ops.conv2d(self._pc2, ha, pad=cp, residual=ops.conv2d(self._pcs, x), gn_stats=True)

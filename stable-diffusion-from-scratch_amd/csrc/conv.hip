@@ -2146,6 +2146,22 @@ __global__ void __launch_bounds__(512) conv_ph_kernel(Params p) {
     return;
   }
   if (p.split == 1 && (p.out_mode == SDK_OUT_NHWC_F16 || p.out_mode == SDK_OUT_GEGLU_F16)) {
+    if (p.gnp) {
+      // GroupNorm statistics of the stored tile (build_params: full fp16 NHWC tiles only): each of the
+      // two 128-row halves gets its own per-wave scratch + parked (mean, M2) [2][64] (5.5 KiB per wave,
+      // 16 areas in the idle ring), then one thread per tile channel merges the 8 row blocks of 32 —
+      // "virtual" wave rows 2 * half + wr in row order
+      constexpr int PWS = (EPI_BYTES + 2 * 64 * 8) / 2;   // halfs per scratch area
+      static_assert(16 * PWS * 2 <= PC::RING_BYTES, "GN scratch fits the ring");
+      epilogue_lds<2, 2, true>(p, acc[0], m0, n0, wr * 64, wc * 64, lds + wave * PWS, bias_s, rb_s);
+      epilogue_lds<2, 2, true>(p, acc[1], m0, n0, 128 + wr * 64, wc * 64, lds + (8 + wave) * PWS, bias_s, rb_s);
+      __syncthreads();
+      gn_tile_store<4, 4, 64, 2, 32, 256, 256>(p, m0, n0, [&](int w) {
+        const int vm = w >> 2, wn = w & 3;   // virtual wave row = 2 * half + wr
+        return reinterpret_cast<const float2*>(lds + ((vm >> 1) * 8 + (vm & 1) * 4 + wn) * PWS + EPI_BYTES / 2);
+      });
+      return;
+    }
     epilogue_lds<2, 2>(p, acc[0], m0, n0, wr * 64, wc * 64, lds + wave * (EPI_BYTES / 2), bias_s, rb_s);
     epilogue_lds<2, 2>(p, acc[1], m0, n0, 128 + wr * 64, wc * 64, lds + wave * (EPI_BYTES / 2), bias_s, rb_s);
   } else {
@@ -2911,8 +2927,8 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   // GroupNorm statistics of the output: chunks per image the plan can emit (0 = none).  Split-K: the
   // reduce kernel, 64-row chunks (one chunk when hw_out is not a multiple of 64); otherwise the
   // LDS-DMA kernels' fp16 epilogue, one chunk per M-tile when tiles do not straddle images.
-  const bool glds = (var >= 2 && var <= 7) || (var >= 16 && var <= 19) || (var >= 22 && var <= 26) ||
-                    (var >= 31 && var <= 33);
+  const bool glds = (var >= 2 && var <= 9) || (var >= 16 && var <= 19) || (var >= 22 && var <= 26) ||
+                    (var >= 31 && var <= 33);   // 8 / 9: the phased kernel's 32x32x16 epilogue
   int gn_nch = 0;
   if (a->out_mode == SDK_OUT_NHWC_F16) {
     if (split > 1) gn_nch = p.hw_out % 64 == 0 ? p.hw_out / 64 : 1;

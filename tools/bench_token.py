@@ -30,6 +30,13 @@ def main():
             nb = M * 320 * 2 * (3 if res is not None else 2)
             print(f"M={M} {tag:12s}: tiled {t0:6.1f} us  token {t1:6.1f} us  ({nb / t1 / 1e3:.0f} GB/s algorithmic)",
                   flush=True)
+        g = torch.ones(320, device=dev)
+        bt = torch.zeros(320, device=dev)
+        t0 = graph_us(lambda: ops.layer_norm(ops.linear(pc, x), g, bt, 1e-5))
+        t1 = graph_us(lambda: ops.token_linear(pk, x, norm=(g, bt, 1e-5)))
+        nb = M * 320 * 2 * 3
+        print(f"M={M} {'+ norm':12s}: tiled+LN {t0:6.1f} us  token_ln {t1:6.1f} us  ({nb / t1 / 1e3:.0f} GB/s algorithmic)",
+              flush=True)
 
 
 if __name__ == "__main__":
