@@ -101,11 +101,20 @@ TOKEN_LINEAR = os.environ.get("SD_AMD_TOKEN_LINEAR", "1") != "0"
 
 class ReassocContext:
     """A prompt batch's cross-attention operands: the K|V projection (the three-launch path) and the
-    per-prompt reassociated GEMM weights."""
-    __slots__ = ("kv", "w1", "w2", "heads", "nk")
+    per-prompt reassociated GEMM weights, built on first use by a block whose token count takes the
+    reassociated path (N % 128 == 0) — the 8x8 middle block of SD-1 at 512^2 never builds them.
+    Built outside any graph capture: GraphedUNet runs one eager evaluation before it captures."""
+    __slots__ = ("kv", "w1", "w2", "heads", "nk", "batch", "_build")
 
-    def __init__(self, kv, w1, w2, heads, nk):
-        self.kv, self.w1, self.w2, self.heads, self.nk = kv, w1, w2, heads, nk
+    def __init__(self, kv, heads, nk, batch, build):
+        self.kv, self.heads, self.nk, self.batch, self._build = kv, heads, nk, batch, build
+        self.w1 = self.w2 = None
+
+    def weights(self):
+        if self.w1 is None:
+            self.w1, self.w2 = self._build()
+            self._build = None
+        return self.w1, self.w2
 
 
 def reassoc_weights(k, v, wq, wo):
@@ -169,15 +178,18 @@ class CrossAttention(nn.Module):
         B, H, d = ctx2d.shape[0] // L, self.heads, self.dim_head
         C = self.to_q.in_features
         Co = self.to_out[0].out_features
-        kr = (H * L + ops.BK - 1) // ops.BK * ops.BK
-        k = kv[:, :inner].float().view(B, L, H, d)
-        v = kv[:, inner:].float().view(B, L, H, d)
-        r1, r2 = reassoc_weights(k, v, self._wq32, self._wo32)
-        w1 = torch.zeros(B, (kr + ops.BN - 1) // ops.BN * ops.BN, C, dtype=torch.float16, device=kv.device)
-        w1[:, :H * L] = r1.half()
-        w2 = torch.zeros(B, (Co + ops.BN - 1) // ops.BN * ops.BN, kr, dtype=torch.float16, device=kv.device)
-        w2[:, :Co, :H * L] = r2.half()
-        return ReassocContext(kv, ops.PerImageWeights(w1, H * L), ops.PerImageWeights(w2, Co, self._bo32), H, L)
+
+        def build():
+            kr = (H * L + ops.BK - 1) // ops.BK * ops.BK
+            k = kv[:, :inner].float().view(B, L, H, d)
+            v = kv[:, inner:].float().view(B, L, H, d)
+            r1, r2 = reassoc_weights(k, v, self._wq32, self._wo32)
+            w1 = torch.zeros(B, (kr + ops.BN - 1) // ops.BN * ops.BN, C, dtype=torch.float16, device=kv.device)
+            w1[:, :H * L] = r1.half()
+            w2 = torch.zeros(B, (Co + ops.BN - 1) // ops.BN * ops.BN, kr, dtype=torch.float16, device=kv.device)
+            w2[:, :Co, :H * L] = r2.half()
+            return ops.PerImageWeights(w1, H * L), ops.PerImageWeights(w2, Co, self._bo32)
+        return ReassocContext(kv, H, L, B, build)
 
     def _run(self, t, residual, B, N, kv=None, Lc=None):
         inner = self.heads * self.dim_head
@@ -195,10 +207,11 @@ class CrossAttention(nn.Module):
             # where the shape is supported, else the three launches
             ops.PROFILER.region = "cross_attention"
             if isinstance(kv, ReassocContext):
-                if t.stride(-1) == 1 and N % 128 == 0 and kv.w1.weight.shape[0] == B:
-                    s = ops.linear(kv.w1, t, out_mode=ops.OUT_ROWS_F32, n_img=N)
-                    p = ops.segment_softmax(s, kv.heads, kv.nk, self.scale, ld_p=kv.w2.k_total)
-                    out = ops.linear(kv.w2, p, residual=residual, n_img=N)
+                if t.stride(-1) == 1 and N % 128 == 0 and kv.batch == B:
+                    w1, w2 = kv.weights()
+                    s = ops.linear(w1, t, out_mode=ops.OUT_ROWS_F32, n_img=N)
+                    p = ops.segment_softmax(s, kv.heads, kv.nk, self.scale, ld_p=w2.k_total)
+                    out = ops.linear(w2, p, residual=residual, n_img=N)
                     ops.PROFILER.region = None
                     return out
                 kv = kv.kv

@@ -79,7 +79,12 @@ def test_reassociated_cross_attention_block(sdk, ops, B):
     res = torch.randn(B * N, C).half()
     kvr = att.context_kv(ctx.to(DEV), L)
     assert isinstance(kvr, ReassocContext)
+    # a block at the 8x8 level (64 tokens: not the reassociated path) builds no per-prompt matrices
+    t64 = torch.randn(B * 64, C).half().to(DEV)
+    att._run(t64, t64, B, 64, kvr, L)
+    assert kvr.w1 is None and kvr.w2 is None
     y_re = att._run(t.to(DEV), res.to(DEV), B, N, kvr, L).float().cpu()
+    assert kvr.w1 is not None
     y_3 = att._run(t.to(DEV), res.to(DEV), B, N, kvr.kv, L).float().cpu()
     # fp32 reference on the same fp16 inputs and weights
     wq, wk, wv = (m.weight.detach().float().cpu() for m in (att.to_q, att.to_k, att.to_v))
