@@ -48,6 +48,7 @@ __device__ __forceinline__ void stamp(const XAttnParams& p, int i) {
 unsigned long long* g_xattn_stamps = nullptr;
 
 typedef _Float16 h4v __attribute__((ext_vector_type(4)));
+typedef __fp16 fp16x4_t __attribute__((ext_vector_type(4)));
 
 constexpr int XQ = 64;     // query rows per workgroup
 constexpr int XKP = 80;    // key slots (5 blocks of 16)
@@ -62,8 +63,12 @@ struct XCfg {
   static constexpr int WP = C <= 320 ? 3 : 4;      // W prefetch depth (K-steps): 320 keeps 2 waves / SIMD
   static constexpr int QLD = C + 8;                 // q / o row stride (halfs); 8 zero pad columns
   static constexpr int KLD = DP + 8;                // K rows [key][d]
-  static constexpr int VLD = XKP + 8;               // V^T rows [d][key]
-  static constexpr int KVH = XKP * KLD + DP * VLD;  // one head's K + V^T (halfs)
+  // V rows [key][d] (row-major, 16-B copies like K; the PV operand V^T is read with ds_read_b64_tr_b16):
+  // VLD / 2 = 8 * odd (mod 64) dwords puts the 8 rows of a transposed read's 32-lane half on 8 disjoint
+  // 8-bank spans (conflict-free): DP = 48 and 80 qualify, DP = 64 takes 80
+  static constexpr int VLD = (DP / 2) % 16 == 8 ? DP : DP + 16;
+  static_assert((VLD / 2) % 16 == 8, "V row stride: conflict-free transposed reads");
+  static constexpr int KVH = XKP * KLD + XKP * VLD; // one head's K + V (halfs)
   // heads per iteration: 2 where the second K / V^T buffer keeps the resident group count
   static constexpr int ONE = (XQ * QLD + KVH) * 2, TWO = (XQ * QLD + 2 * KVH) * 2;
   static constexpr int HPI = (TWO <= 80 * 1024 || ONE > 80 * 1024) && H > 1 ? 2 : 1;
@@ -170,7 +175,7 @@ __global__ void __launch_bounds__(256, 1) xattn_block_kernel(XAttnParams p) {
   using X = XCfg<C, D>;
   extern __shared__ __attribute__((aligned(16))) half_t xl[];
   half_t* qo = xl;                              // [64][QLD]
-  half_t* kvl = qo + XQ * X::QLD;               // HPI x { K [80][KLD], V^T [DP][VLD] }
+  half_t* kvl = qo + XQ * X::QLD;               // HPI x { K [80][KLD], V [80][VLD] }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r16 = lane & 15, c16 = lane >> 4;
   const int m0 = blockIdx.x * XQ;
@@ -268,15 +273,14 @@ __global__ void __launch_bounds__(256, 1) xattn_block_kernel(XAttnParams p) {
 #pragma unroll
     for (int g = 0; g < HPI; ++g) {
       half_t* kl = kvl + g * X::KVH;
-      half_t* vt = kl + XKP * X::KLD;
+      half_t* vr = kl + XKP * X::KLD;
 #pragma unroll
       for (int u = 0; u < NCH; ++u) {
         const int e = tid + 256 * u;
         const int key = e / CH, ch = e - key * CH;
         if (key < p.nk && it * HPI + g < X::H) {
           *reinterpret_cast<h8*>(kl + key * X::KLD + 8 * ch) = rk[sl][g][u];
-#pragma unroll
-          for (int q = 0; q < 8; ++q) vt[(8 * ch + q) * X::VLD + key] = rv[sl][g][u][q];
+          *reinterpret_cast<h8*>(vr + key * X::VLD + 8 * ch) = rv[sl][g][u];
         }
       }
     }
@@ -345,18 +349,24 @@ __global__ void __launch_bounds__(256, 1) xattn_block_kernel(XAttnParams p) {
       sum[g] += __shfl_xor(sum[g], 32, 64);
       inv[g] = 1.f / sum[g];
     }
-    // O^T[d, q] = sum_key V^T[d, key] P^T[key, q]
+    // O^T[d, q] = sum_key V^T[d, key] P^T[key, q]; the A operand V^T[dd + i][16 kb + 4 g' + q] comes from the
+    // row-major V by the hardware transposed read: lane 4 q + pp of 16-lane group g' supplies the address of
+    // V[16 kb + 4 g' + q][dd + 4 pp .. + 3] and receives column dd + (lane & 15) of the group's 4 rows
+    // (EXEC is all ones here: g < ng is wave-uniform)
+    const int tr_off = (4 * c16 + ((lane & 15) >> 2)) * X::VLD + 4 * (lane & 3);
 #pragma unroll
     for (int g = 0; g < HPI; ++g) {
       if (g < ng) {
         const int h = it * HPI + g;
-        const half_t* vt = kvl + g * X::KVH + XKP * X::KLD;
+        const half_t* vr = kvl + g * X::KVH + XKP * X::KLD;
 #pragma unroll
         for (int dd = 0; dd < X::DP; dd += 16) {
           f4 o = f4{};
 #pragma unroll
           for (int kb = 0; kb < XKP / 16; ++kb) {
-            const h4v fv = *reinterpret_cast<const h4v*>(vt + (dd + r16) * X::VLD + 16 * kb + 4 * c16);
+            const auto t4 = __builtin_amdgcn_ds_read_tr16_b64_v4f16(
+                (__attribute__((address_space(3))) fp16x4_t*)(vr + 16 * kb * X::VLD + dd + tr_off));
+            const h4v fv = __builtin_bit_cast(h4v, t4);
             o = __builtin_amdgcn_mfma_f32_16x16x16f16(fv, pf[g][kb], o, 0, 0, 0);
           }
           const int d0 = dd + 4 * c16;          // lane holds d0..d0+3 of query qrow
