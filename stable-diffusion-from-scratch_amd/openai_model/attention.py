@@ -118,9 +118,11 @@ class ReassocContext:
 
 
 def reassoc_weights(k, v, wq, wo):
-    """fp32 per-prompt matrices of the reassociated block: k, v [B, L, H, d] (the context K / V),
-    wq [H*d, C] (to_q.weight), wo [Co, H*d] (to_out.weight) -> w1 [B, H*L, C] with
-    w1[b, h*L + j] = K[b, j, h] Wq_h, and w2 [B, Co, H*L] with w2[b, :, h*L + j] = Wo_h V[b, j, h]^T."""
+    """The per-prompt matrices of the reassociated block as math (the CPU statement the tests check the
+    regrouping with; the device path computes the same products per head on sdk_conv2d, see
+    CrossAttention.context_kv): k, v [B, L, H, d] (the context K / V), wq [H*d, C] (to_q.weight),
+    wo [Co, H*d] (to_out.weight) -> w1 [B, H*L, C] with w1[b, h*L + j] = K[b, j, h] Wq_h, and
+    w2 [B, Co, H*L] with w2[b, :, h*L + j] = Wo_h V[b, j, h]^T."""
     B, L, H, d = k.shape
     w1 = torch.einsum("bjhe,hec->bhjc", k, wq.view(H, d, -1)).reshape(B, H * L, -1)
     w2 = torch.einsum("che,bjhe->bchj", wo.view(wo.shape[0], H, d), v).reshape(B, wo.shape[0], H * L)
@@ -164,9 +166,8 @@ class CrossAttention(nn.Module):
         self._ptl_o = (ops.PackedTokenLinear(self.to_out[0].weight, self.to_out[0].bias, dev)
                        if self.self_attn and ops.token_linear_supported(inner, self.to_out[0].out_features) else None)
         if not self.self_attn:
-            self._wq32 = self.to_q.weight.detach().to(dev, torch.float32)          # [inner, C]
-            self._wo32 = self.to_out[0].weight.detach().to(dev, torch.float32)     # [C, inner]
             self._bo32 = self.to_out[0].bias.detach().to(dev, torch.float32).contiguous()
+            self._pc_reassoc = None    # per-head GEMM weights of the reassociated per-prompt matrices (lazy)
 
     def context_kv(self, ctx2d, L=None):
         """K|V of the conditioning, [B*L, 2*inner] — computed once per conditioning tensor; with ``L``
@@ -180,14 +181,24 @@ class CrossAttention(nn.Module):
         Co = self.to_out[0].out_features
 
         def build():
+            # per head h, on the library GEMM (sdk_conv2d, fp32 accumulation, fp16 out like the stored
+            # matrices): K_h Wq_h = K_h [B*L, d] x (Wq_h^T as an [C, d] weight) and
+            # (Wo_h V_h^T)^T = V_h [B*L, d] x (Wo_h as a [Co, d] weight); reassoc_weights is the same math
+            dev = kv.device
+            if self._pc_reassoc is None:
+                wq, wo = self.to_q.weight.detach(), self.to_out[0].weight.detach()
+                self._pc_reassoc = (
+                    [ops.PackedConv([(wq[h * d:(h + 1) * d].t().contiguous(), d)], None, device=dev) for h in range(H)],
+                    [ops.PackedConv([(wo[:, h * d:(h + 1) * d].contiguous(), d)], None, device=dev) for h in range(H)])
+            pq, po = self._pc_reassoc
             kr = (H * L + ops.BK - 1) // ops.BK * ops.BK
-            k = kv[:, :inner].float().view(B, L, H, d)
-            v = kv[:, inner:].float().view(B, L, H, d)
-            r1, r2 = reassoc_weights(k, v, self._wq32, self._wo32)
-            w1 = torch.zeros(B, (kr + ops.BN - 1) // ops.BN * ops.BN, C, dtype=torch.float16, device=kv.device)
-            w1[:, :H * L] = r1.half()
-            w2 = torch.zeros(B, (Co + ops.BN - 1) // ops.BN * ops.BN, kr, dtype=torch.float16, device=kv.device)
-            w2[:, :Co, :H * L] = r2.half()
+            w1 = torch.zeros(B, (kr + ops.BN - 1) // ops.BN * ops.BN, C, dtype=torch.float16, device=dev)
+            w2 = torch.zeros(B, (Co + ops.BN - 1) // ops.BN * ops.BN, kr, dtype=torch.float16, device=dev)
+            w1h = w1[:, :H * L].view(B, H, L, C)
+            for h in range(H):
+                w1h[:, h] = ops.linear(pq[h], kv[:, h * d:(h + 1) * d]).view(B, L, C)
+                w2[:, :Co, h * L:(h + 1) * L] = ops.linear(po[h], kv[:, inner + h * d:inner + (h + 1) * d]).view(
+                    B, L, Co).transpose(1, 2)
             return ops.PerImageWeights(w1, H * L), ops.PerImageWeights(w2, Co, self._bo32)
         return ReassocContext(kv, H, L, B, build)
 
