@@ -106,7 +106,15 @@ typedef struct {
                                    weight + b * weight_batch_stride (elements); only the LDS-DMA tile
                                    kernels, with M-tiles inside one image (the reassociated
                                    cross-attention's per-prompt matrices) */
+  int32_t split_inlaunch;  /* 1: split_k must be 2 and the plan an LDS-DMA tile kernel; the two K halves of a
+                              tile are combined INSIDE the launch (each writes its fp32 accumulator blob to the
+                              workspace; the second to arrive adds the first's and runs the full epilogue,
+                              GroupNorm statistics included): no reduce kernel, no slab round trip through it */
+  uint32_t* tile_counters; /* with split_inlaunch: >= SDK_TILE_COUNTERS zero-initialised words, one arrival
+                              counter per output tile (device memory); every launch leaves them zero */
 } sdk_conv_args;
+
+#define SDK_TILE_COUNTERS 16384
 
 enum sdk_conv_act {
   SDK_ACT_NONE = 0,

@@ -29,7 +29,8 @@ class ConvArgs(C.Structure):
                 ("weight", vp), ("k_total", i32), ("bias", vp), ("row_bias", vp), ("row_bias_ld", i32),
                 ("residual", vp), ("res_ld", i32), ("out", vp), ("out_ld", i32), ("out_mode", i32),
                 ("split_k", i32), ("workspace", vp), ("workspace_bytes", i64), ("variant_hint", i32),
-                ("act", i32), ("gn_partial", vp), ("weight_batch_stride", i64)]
+                ("act", i32), ("gn_partial", vp), ("weight_batch_stride", i64), ("split_inlaunch", i32),
+                ("tile_counters", vp)]
 
 
 class ConvPlanInfo(C.Structure):

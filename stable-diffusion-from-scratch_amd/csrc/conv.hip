@@ -77,6 +77,10 @@ struct Params {
   // GroupNorm scale / shift (seg[0].gscale / gshift, [batch][cin]) and SiLU applied to each staged piece
   // in LDS; halo row of pixel h = (h * h_divm) >> 20 (exact for the plan's pixel range)
   int h_virt, h_divm;
+  // in-launch split-K (LDS-DMA tile kernels, split == 2): the K halves of a tile combine inside the launch;
+  // partial = one fp32 accumulator blob per (tile, half), tcnt = per-tile arrival counters (left zero)
+  int inl;
+  unsigned* tcnt;
 };
 
 // epilogue activation (CLIP's quick_gelu x*sigmoid(1.702x), transformers activations.py QuickGELUActivation)
@@ -425,7 +429,7 @@ __device__ __forceinline__ void epilogue_direct(const Params& p, f16v (&acc)[FM]
     const int m = m0 + m_w + i * 32 + fr;
     if (m >= p.M) continue;
     const int b = m / p.hw_out;
-    if (p.split > 1) {
+    if (p.split > 1 && !p.inl) {
       float* slab = p.partial + ((size_t)split_idx * p.M + m) * p.Npad;
 #pragma unroll
       for (int j = 0; j < FN; ++j)
@@ -971,7 +975,7 @@ __device__ __forceinline__ void epilogue16_tile_direct(const Params& p, f4 (&acc
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int n = n0 + n_w + 16 * j + 4 * cg;
-      if (p.split > 1) {
+      if (p.split > 1 && !p.inl) {
         *reinterpret_cast<f4*>(p.partial + ((size_t)split_idx * p.M + m) * p.Npad + n) = acc[i][j];
         continue;
       }
@@ -1176,7 +1180,7 @@ __device__ __forceinline__ EpiVec epi_vec_load(const Params& p, int m0, int n0, 
   const int tid = threadIdx.x;
   EpiVec e{0.f, 0.f, false};
   const int b0 = m0 / p.hw_out;
-  e.one_img = p.row_bias && p.split == 1 && b0 == (min(m0 + tbm, p.M) - 1) / p.hw_out;
+  e.one_img = p.row_bias && (p.split == 1 || p.inl) && b0 == (min(m0 + tbm, p.M) - 1) / p.hw_out;
   if (tid < tbn && n0 + tid < p.N) {
     if (p.bias) e.bias = p.bias[n0 + tid];
     if (e.one_img) e.rb = p.row_bias[(size_t)b0 * p.rb_ld + n0 + tid];
@@ -1199,6 +1203,13 @@ __device__ __forceinline__ void epi_vec_store(const EpiVec& e, float* vec_s, int
 // is the large operand: (N-tile, K-slice) major, M-tile minor, so the M-tiles that read one weight
 // slice are co-resident on an XCD and the slice comes from L2 instead of once per M-tile.
 __device__ __forceinline__ void item_coords(const Params& p, int it, int& tm, int& tn, int& sidx) {
+  if (p.inl) {   // the two halves of a tile are neighbouring items (one XCD under xcd_remap)
+    const int t = it >> 1;
+    sidx = it & 1;
+    tm = t / p.tiles_n;
+    tn = t - tm * p.tiles_n;
+    return;
+  }
   if (p.split == 1) {
     tm = it / p.tiles_n;
     tn = it - tm * p.tiles_n;
@@ -1348,6 +1359,70 @@ __global__ void __launch_bounds__(CF::NT, CF::OCC * CF::NW / 4) conv_glds_kernel
 #undef SDK_STAGE
   // the trailing zero-page DMAs land before the ring is reused as epilogue scratch
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (p.inl) {
+    // in-launch split-K: both halves dump their accumulators as a lane-major blob (16-B stores, every wave
+    // instruction a contiguous KiB), publish with an agent-scope release and take a ticket; the second
+    // arrival acquires, adds the other half's blob and runs the epilogue as an unsplit tile
+    // (cdna_hip_programming.md §5 'In-launch split-K reduction').  fp32 a + b == b + a: the sum is the
+    // same whichever half arrives last.
+    constexpr int NQ = CF::M16 ? CF::FM16 * CF::FN16 : CF::FM * CF::FN * 4;   // f4 groups per thread
+    const int tile = tm * p.tiles_n + tn;
+    f4* mine = reinterpret_cast<f4*>(p.partial) + ((size_t)tile * 2 + sidx) * NQ * CF::NT + tid;
+    const f4* other = reinterpret_cast<const f4*>(p.partial) + ((size_t)tile * 2 + (sidx ^ 1)) * NQ * CF::NT + tid;
+    if constexpr (CF::M16) {
+#pragma unroll
+      for (int i = 0; i < CF::FM16; ++i)
+#pragma unroll
+        for (int j = 0; j < CF::FN16; ++j) mine[(i * CF::FN16 + j) * CF::NT] = acc16[i][j];
+    } else {
+#pragma unroll
+      for (int i = 0; i < CF::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < CF::FN; ++j)
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            mine[((i * CF::FN + j) * 4 + g) * CF::NT] =
+                f4{acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    unsigned* flag = reinterpret_cast<unsigned*>(lds);   // the ring is idle: every wave is past its last read
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned ticket = __hip_atomic_fetch_add(p.tcnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (ticket == 1) {
+        __hip_atomic_store(p.tcnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // left zero
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      *flag = ticket;
+    }
+    __syncthreads();
+    if (*flag != 1) return;
+    __syncthreads();   // every wave read the flag before the ring becomes epilogue scratch
+    if constexpr (CF::M16) {
+#pragma unroll
+      for (int i = 0; i < CF::FM16; ++i)
+#pragma unroll
+        for (int j = 0; j < CF::FN16; ++j) {
+          const f4 o = other[(i * CF::FN16 + j) * CF::NT];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc16[i][j][r] += o[r];
+        }
+    } else {
+#pragma unroll
+      for (int i = 0; i < CF::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < CF::FN; ++j)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f4 o = other[((i * CF::FN + j) * 4 + g) * CF::NT];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[i][j][4 * g + r] += o[r];
+          }
+    }
+  }
   float* vec_s = reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + CF::RING_BYTES);
   epi_vec_store(ev, vec_s, CF::TBN);
   __builtin_amdgcn_s_barrier();
@@ -1355,7 +1430,7 @@ __global__ void __launch_bounds__(CF::NT, CF::OCC * CF::NW / 4) conv_glds_kernel
   const float* rb_s = ev.one_img ? vec_s + CF::TBN : nullptr;
   constexpr int WSCR = CF::RING_BYTES / CF::NW / 16 * 8;   // per-wave epilogue scratch (halfs)
   half_t* wscr = lds + wave * WSCR;
-  const bool lds_epi = p.split == 1 && (p.out_mode == SDK_OUT_NHWC_F16 || p.out_mode == SDK_OUT_GEGLU_F16);
+  const bool lds_epi = (p.split == 1 || p.inl) && (p.out_mode == SDK_OUT_NHWC_F16 || p.out_mode == SDK_OUT_GEGLU_F16);
   // the tile's GroupNorm statistics (build_params enables p.gnp for full fp16 NHWC tiles only)
   auto gn_store = [&](int scratch_halfs, auto blk_rows) __attribute__((always_inline)) {
     constexpr int BR = decltype(blk_rows)::value;
@@ -2912,7 +2987,19 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   p.kt_per_split = (kt + split - 1) / split;
   split = (kt + p.kt_per_split - 1) / p.kt_per_split;
   p.split = split;
-  const int64_t ws = split > 1 ? (int64_t)split * p.M * p.Npad * 4 : 0;
+  int64_t ws = split > 1 ? (int64_t)split * p.M * p.Npad * 4 : 0;
+  if (a->split_inlaunch) {
+    const bool tile_kernel = (var >= 2 && var <= 7) || (var >= 16 && var <= 19) || (var >= 22 && var <= 26) ||
+                             (var >= 31 && var <= 33);
+    if (!tile_kernel)
+      return fail(SDK_EINVAL, "conv2d: in-launch split-K needs an LDS-DMA tile plan (variants 2-7, 16-19, 22-26, 31-33)");
+    if (split != 2) return fail(SDK_EINVAL, "conv2d: in-launch split-K combines exactly two K halves (split_k = 2)");
+    if (!a->tile_counters) return fail(SDK_EINVAL, "conv2d: in-launch split-K needs tile_counters");
+    if (tiles > SDK_TILE_COUNTERS) return fail(SDK_EINVAL, "conv2d: in-launch split-K: more tiles than counters");
+    p.inl = 1;
+    p.tcnt = a->tile_counters;
+    ws = (int64_t)2 * tiles * tbm * tbn * 4;   // one fp32 accumulator blob per (tile, half)
+  }
   if (info) {
     info->split_k = split;
     info->grid_tiles = tiles;
@@ -2931,8 +3018,8 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
                     (var >= 31 && var <= 33);   // 8 / 9: the phased kernel's 32x32x16 epilogue
   int gn_nch = 0;
   if (a->out_mode == SDK_OUT_NHWC_F16) {
-    if (split > 1) gn_nch = p.hw_out % 64 == 0 ? p.hw_out / 64 : 1;
-    else if (glds && p.hw_out % tbm == 0) gn_nch = p.hw_out / tbm;
+    if (split > 1 && !p.inl) gn_nch = p.hw_out % 64 == 0 ? p.hw_out / 64 : 1;
+    else if (glds && p.hw_out % tbm == 0) gn_nch = p.hw_out / tbm;   // in-launch split: the combining tile emits
   }
   if (info) info->gn_chunks = gn_nch;
   if (a->gn_partial) {
@@ -3009,6 +3096,7 @@ extern "C" int sdk_conv2d(const sdk_conv_args* a, sdk_stream_t stream) {
       rc = check_launch("conv_igemm");
   }
   if (rc) return rc;
+  if (p.inl) return SDK_OK;   // combined inside the launch
   if (p.split > 1 && p.gnp) {
     hipLaunchKernelGGL(splitk_reduce_gn_kernel, dim3(p.batch * p.gn_nch, (p.N + 63) / 64), dim3(256), 0, s, p);
     if (int e = check_launch("splitk_reduce_gn")) return e;

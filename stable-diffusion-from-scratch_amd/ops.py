@@ -70,6 +70,18 @@ class _Workspace:
                 self.lane = prev
         return cm()
 
+    def counters(self, device) -> torch.Tensor:
+        """The lane's per-tile arrival counters of in-launch split-K convs: zeroed once, and every launch
+        leaves them zero (its last arrival resets each), so one fixed buffer serves every call of the lane."""
+        key = (torch.device(device).index, self.lane, "cnt")
+        c = self.buf.get(key)
+        if c is None:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("sd_amd: tile counters must exist before graph capture (run one warm-up step)")
+            c = torch.zeros(TILE_COUNTERS, dtype=torch.int32, device=device)
+            self.buf[key] = c
+        return c
+
     def get(self, nbytes: int, device) -> torch.Tensor:
         key = (torch.device(device).index, self.lane)
         b = self.buf.get(key)
@@ -85,6 +97,7 @@ class _Workspace:
 
 
 WORKSPACE = _Workspace()
+TILE_COUNTERS = 16384     # sdk_amd.h SDK_TILE_COUNTERS
 
 
 # --------------------------------------------------------------------------- sources
@@ -218,7 +231,8 @@ class _Autotune:
     first call of each distinct problem times every candidate (HIP events, 3 reps
     after a warm-up; SD_AMD_TUNE_REPS) and caches the fastest.  Never runs under graph capture."""
     VARIANTS = (2, 5, 7, 6, 4, 3, 8, 9, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 31, 32, 33, 34, 35, 36, 37)
-    SPLITS = (0, 1, 2, 4, 8)
+    # split -2: two K halves combined inside the launch (sdk_conv_args.split_inlaunch; LDS-DMA tile kernels)
+    SPLITS = (0, 1, 2, 4, 8, -2)
 
     def __init__(self):
         import os
@@ -283,12 +297,14 @@ class _Autotune:
         if gn:                           # is there a candidate at all that emits the statistics?
             for v in cands:
                 for sp in self.SPLITS:
-                    a.variant_hint, a.split_k = v + 1, sp
+                    a.variant_hint = v + 1
+                    set_split(a, sp, dev)
                     if lib().sdk_conv2d_plan(C.byref(a), C.byref(info)) == 0 and info.gn_chunks > 0:
                         emit_any = True
         for v in cands:
             for sp in self.SPLITS:
-                a.variant_hint, a.split_k = v + 1, sp
+                a.variant_hint = v + 1
+                set_split(a, sp, dev)
                 if lib().sdk_conv2d_plan(C.byref(a), C.byref(info)) != 0:
                     continue
                 if info.variant != v:
@@ -315,8 +331,9 @@ class _Autotune:
                 e1.synchronize()
                 t = e0.elapsed_time(e1)
                 if t < best_t:
-                    best_t, best = t, (v + 1, info.split_k)
-        a.variant_hint, a.split_k, a.gn_partial = 0, 0, None
+                    best_t, best = t, (v + 1, -2 if sp == -2 else info.split_k)
+        a.variant_hint, a.gn_partial = 0, None
+        set_split(a, 0, dev)
         self.table[key] = best
         self.timed += 1
         if self.timed % 10 == 0:             # progress (a full re-tune takes minutes)
@@ -326,6 +343,16 @@ class _Autotune:
 
 
 AUTOTUNE = _Autotune()
+
+
+def set_split(a, sp, dev):
+    """split_k of a ConvArgs; ``sp == -2`` requests the in-launch combine of two K halves (its arrival
+    counters: ``WORKSPACE.counters``)."""
+    if sp == -2:
+        a.split_k, a.split_inlaunch = 2, 1
+        a.tile_counters = WORKSPACE.counters(dev).data_ptr()
+    else:
+        a.split_k, a.split_inlaunch, a.tile_counters = sp, 0, None
 
 
 # tests / benchmarks: force one tile configuration on every conv call (None = planner / autotuner)
@@ -462,13 +489,14 @@ def conv2d(pc: PackedConv, x, *, ksize=None, stride=1, pad=None, pad_end=0, upsa
     want_gn = gn_stats and EMIT_GN_STATS and out_mode == OUT_NHWC_F16
     tuned = AUTOTUNE.choose(a, pc, dev, want_gn) if (AUTOTUNE.enabled or AUTOTUNE.table) else None
     if tuned is not None:
-        a.variant_hint, a.split_k = tuned
+        a.variant_hint = tuned[0]
+        set_split(a, tuned[1], dev)
     if variant is None:
         variant = FORCE_VARIANT
     if variant is not None:
         a.variant_hint = variant + 1
     if split_k is not None:
-        a.split_k = split_k
+        set_split(a, split_k, dev)    # -2: the in-launch combine of two K halves
     info = ConvPlanInfo()
     check(lib().sdk_conv2d_plan(C.byref(a), C.byref(info)), "conv2d_plan")
     if info.workspace_bytes > 0:
