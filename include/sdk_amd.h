@@ -112,6 +112,10 @@ typedef struct {
                               GroupNorm statistics included): no reduce kernel, no slab round trip through it */
   uint32_t* tile_counters; /* with split_inlaunch: >= SDK_TILE_COUNTERS zero-initialised words, one arrival
                               counter per output tile (device memory); every launch leaves them zero */
+  int32_t tile_group_m;    /* unsplit LDS-DMA / phased / halo plans: output tiles are visited in groups of this
+                              many M-panels, N-tile major inside a group, so the tiles co-resident on one XCD
+                              share both their A panels and their W tiles in its L2; 0: the library's choice,
+                              1: M-panel major (every N-tile of a panel, then the next panel) */
 } sdk_conv_args;
 
 #define SDK_TILE_COUNTERS 16384

@@ -30,7 +30,7 @@ class ConvArgs(C.Structure):
                 ("residual", vp), ("res_ld", i32), ("out", vp), ("out_ld", i32), ("out_mode", i32),
                 ("split_k", i32), ("workspace", vp), ("workspace_bytes", i64), ("variant_hint", i32),
                 ("act", i32), ("gn_partial", vp), ("weight_batch_stride", i64), ("split_inlaunch", i32),
-                ("tile_counters", vp)]
+                ("tile_counters", vp), ("tile_group_m", i32)]
 
 
 class ConvPlanInfo(C.Structure):

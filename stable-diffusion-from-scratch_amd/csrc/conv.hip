@@ -81,6 +81,7 @@ struct Params {
   // partial = one fp32 accumulator blob per (tile, half), tcnt = per-tile arrival counters (left zero)
   int inl;
   unsigned* tcnt;
+  int gm;               // unsplit plans: tiles visited in groups of gm M-panels, N-tile major inside a group
 };
 
 // epilogue activation (CLIP's quick_gelu x*sigmoid(1.702x), transformers activations.py QuickGELUActivation)
@@ -1211,9 +1212,16 @@ __device__ __forceinline__ void item_coords(const Params& p, int it, int& tm, in
     return;
   }
   if (p.split == 1) {
+    sidx = 0;
+    if (p.gm > 1) {   // groups of gm M-panels (the last one shorter), N-tile major inside a group
+      const int gsz = p.gm * p.tiles_n, g = it / gsz, l = it - g * gsz;
+      const int rows = min(p.gm, p.tiles_m - g * p.gm);
+      tn = l / rows;
+      tm = g * p.gm + (l - tn * rows);
+      return;
+    }
     tm = it / p.tiles_n;
     tn = it - tm * p.tiles_n;
-    sidx = 0;
     return;
   }
   const int slab = it / p.tiles_m;
@@ -2667,6 +2675,14 @@ const int g_env_variant = [] {
   return fe ? atoi(fe) : -1;
 }();
 
+// M-panels per tile group of an unsplit plan (item_coords): the caller's value, else M-panel major
+// (SDK_CONV_GM overrides the default, for measurements)
+int tile_group_m(const sdk_conv_args* a, const Params& p) {
+  static const int env_gm = getenv("SDK_CONV_GM") ? atoi(getenv("SDK_CONV_GM")) : 0;
+  const int g = a->tile_group_m > 0 ? a->tile_group_m : env_gm > 0 ? env_gm : 1;
+  return std::max(1, std::min(g, p.tiles_m));
+}
+
 int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   if (!a) return fail(SDK_EINVAL, "conv2d: null args");
   if (a->nseg < 1 || a->nseg > 2) return fail(SDK_EINVAL, "conv2d: nseg must be 1 or 2");
@@ -2903,6 +2919,7 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
       p.kt_per_split = 9 * (((kt + split - 1) / split + 8) / 9);   // split starts on 3x3 channel-block boundaries
       split = (kt + p.kt_per_split - 1) / p.kt_per_split;
       p.split = split;
+      p.gm = split == 1 ? tile_group_m(a, p) : 1;
       const int64_t ws = split > 1 ? (int64_t)split * p.M * p.Npad * 4 : 0;
       int gn_nch = 0;
       if (a->out_mode == SDK_OUT_NHWC_F16) {
@@ -2987,6 +3004,7 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   p.kt_per_split = (kt + split - 1) / split;
   split = (kt + p.kt_per_split - 1) / p.kt_per_split;
   p.split = split;
+  p.gm = split == 1 ? tile_group_m(a, p) : 1;
   int64_t ws = split > 1 ? (int64_t)split * p.M * p.Npad * 4 : 0;
   if (a->split_inlaunch) {
     const bool tile_kernel = (var >= 2 && var <= 7) || (var >= 16 && var <= 19) || (var >= 22 && var <= 26) ||

@@ -357,6 +357,8 @@ def set_split(a, sp, dev):
 
 # tests / benchmarks: force one tile configuration on every conv call (None = planner / autotuner)
 FORCE_VARIANT = None
+# tests / benchmarks: M-panels per tile group of unsplit plans (sdk_conv_args.tile_group_m; None = library default)
+TILE_GROUP_M = None
 
 
 # GroupNorm statistics emitted by the producing conv (tensor attribute; see conv2d(gn_stats=True))
@@ -497,6 +499,8 @@ def conv2d(pc: PackedConv, x, *, ksize=None, stride=1, pad=None, pad_end=0, upsa
         a.variant_hint = variant + 1
     if split_k is not None:
         set_split(a, split_k, dev)    # -2: the in-launch combine of two K halves
+    if TILE_GROUP_M is not None:
+        a.tile_group_m = TILE_GROUP_M
     info = ConvPlanInfo()
     check(lib().sdk_conv2d_plan(C.byref(a), C.byref(info)), "conv2d_plan")
     if info.workspace_bytes > 0:

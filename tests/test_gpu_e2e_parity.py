@@ -8,8 +8,10 @@
   (decode_first_stage).
 * C2 (uncond 256², B = 8): the same 50-step chain on samples 0 and 7 of the bench batch.
 * C5 (SD-2 shape 768², v-prediction, B = 8): one UNet evaluation at the bench batch (tuning table,
-  graph replay) on samples 0 and 7, and the B = 8 decode of images 0 and 7 — a 50-step fp32 chain at
-  96² would take ~6 min of CPU.
+  graph replay) on samples 0 and 7, and the B = 8 decode of images 0 and 7; then the bench's own 50-step
+  v-prediction chain (graph replay) teacher-forced at 3 of its states + the decode of its final latent,
+  and a free-running 10-step v-prediction chain + decode vs the oracle's (a 50-step fp32 chain at 96²
+  would take ~6 min of CPU).
 Every comparison prints and asserts rel-L2 AND max-abs error (relative to the oracle's max-abs); the
 thresholds are ~3x the errors measured on MI355X (profiles/r3_parity_errors.txt)."""
 import os
@@ -161,3 +163,52 @@ def test_c5_bench_batch_unet_and_decode_vs_oracle(sdk):
         _report(f"C5 UNet sample {i} (B=8 bench batch, graph)", y[i:i + 1], ref, 5e-3, 2e-2)
         dref = decode_first_stage(vsd, bench.SD_VAE, z[i:i + 1].cpu(), ld.scale_factor)
         _report(f"C5 decode image {i} (B=8 96->768)", dec[i:i + 1], dref, 5e-3, 2e-2)
+
+
+def test_c5_vpred_chain_vs_oracle(sdk):
+    """C5's v-prediction DDIM chain on the GPU (B=8, tuning table, graph replay at the 96² latent):
+    * the bench step itself (50 steps + decode) is finite and bitwise reproducible, and at 3 states of its
+      own trajectory the GPU's model output (v) matches the oracle UNet's for samples 0 and 7; the decode of
+      its final latent matches the oracle decode;
+    * free-running: a 10-step chain + decode from the same x_T, sample 0, vs the oracle's 10-step chain
+      (``oracle.sampler_ref.ddim_sample(parameterization="v")``; v-pred is parity-unpinned: the reference
+      has no v-prediction)."""
+    from oracle.sampler_ref import ddim_sample
+    from oracle.unet_ref import unet_forward
+    from oracle.vae_ref import decode_first_stage
+    from sd_amd.DDIM.ddim import DDIMSampler
+    bench, cfg, unet, vae, ld, xT, ctx = _bench_models("c5")
+    assert xT.shape[0] == 8 and ld.parameterization == "v"
+    ld.use_graphs(True)
+    sampler = DDIMSampler(ld)
+    step = bench.make_one_step(sampler, ld, xT, ctx, 50, 1, None)
+    img = step().float().cpu()
+    assert img.shape == (8, 3, 768, 768) and torch.isfinite(img).all()
+    z, inter = sampler.sample(S=50, batch_size=8, shape=(4, 96, 96), conditioning=ctx, eta=0.0, x_T=xT,
+                              verbose=False, log_every_t=1)
+    xs = [x.float().cpu().clone() for x in inter["x_inter"]]
+    assert len(xs) == 51
+    assert torch.equal(ld.decode_first_stage(z).float().cpu(), img), "the C5 bench step is deterministic"
+    usd, vsd = _cpu_sd(unet), _cpu_sd(vae)
+    torch.set_num_threads(THREADS)
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from oracle import schedule as sch
+    ts = np.flip(sch.ddim_tables(50, 0.0)["ddim_timesteps"])
+    for i in (0, 25, 49):
+        t = torch.full((8,), int(ts[i]), dtype=torch.long, device=DEV)
+        v_gpu = ld.apply_model(xs[i].to(DEV), t, ctx).float().cpu()
+        for b in (0, 7):
+            v_ref = unet_forward(usd, cfg["unet"], xs[i][b:b + 1], t[b:b + 1].cpu(), ctx[b:b + 1].cpu())
+            _report(f"C5 teacher-forced v at DDIM step {i} (t={int(ts[i])}), sample {b}", v_gpu[b:b + 1], v_ref,
+                    5e-3, 2e-2)
+    dref = decode_first_stage(vsd, bench.SD_VAE, xs[-1][0:1], ld.scale_factor)
+    _report("C5 decode of the GPU's final latent (image 0)", img[0:1], dref, 5e-3, 2e-2)
+    z10, _ = sampler.sample(S=10, batch_size=8, shape=(4, 96, 96), conditioning=ctx, eta=0.0, x_T=xT,
+                            verbose=False, log_every_t=10 ** 9)
+    img10 = ld.decode_first_stage(z10)[0:1].float().cpu()
+    t0 = time.time()
+    fn = lambda x, t: unet_forward(usd, cfg["unet"], x, t, ctx[0:1].cpu())   # noqa: E731
+    zr, _ = ddim_sample(fn, xT[0:1].cpu(), 10, 0.0, parameterization="v")
+    ref10 = decode_first_stage(vsd, bench.SD_VAE, zr, ld.scale_factor)
+    print(f"[parity] C5 10-step oracle chain: {time.time() - t0:.0f} s", flush=True)
+    _report("C5 image 0 free-running (10 v-pred DDIM steps + decode, B=8)", img10, ref10, 8e-3, 2e-2)
