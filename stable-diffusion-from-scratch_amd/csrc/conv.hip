@@ -82,7 +82,18 @@ struct Params {
   int inl;
   unsigned* tcnt;
   int gm;               // unsplit plans: tiles visited in groups of gm M-panels, N-tile major inside a group
+  unsigned long long* stamps;   // diagnostics build only: 8 shader-clock stamps per workgroup, or null
 };
+
+// diagnostics build: s_memtime at kernel entry / after the prologue / after the K loop / at the end (+ after
+// epilogue groups 0-3 at 4-7), by
+// thread 0 of every workgroup (sdk_diag_conv_stamps copies them out); compiled out of the product library
+__device__ __forceinline__ void ph_stamp(const Params& p, int i) {
+#ifdef SDK_CONV_DIAGNOSTICS
+  if (p.stamps && threadIdx.x == 0)
+    p.stamps[((size_t)blockIdx.x + (size_t)blockIdx.y * gridDim.x) * 8 + i] = __builtin_amdgcn_s_memtime();
+#endif
+}
 
 // epilogue activation (CLIP's quick_gelu x*sigmoid(1.702x), transformers activations.py QuickGELUActivation)
 __device__ __forceinline__ float act_fn(int act, float x) {
@@ -96,10 +107,12 @@ __device__ __forceinline__ int swz(int row, int chunk) {   // element offset ins
 
 __device__ __forceinline__ h8 ldg16(const half_t* p) { return *reinterpret_cast<const h8*>(p); }
 
-// fp16 output row stores of the epilogues (SDK_STORE_HINT=1: non-temporal, an A/B build only)
+// fp16 output row stores of the epilogues (SDK_STORE_HINT=1: non-temporal; 2: no store — A/B builds only)
 __device__ __forceinline__ void st_out16(half_t* p, const h8& v) {
 #if defined(SDK_STORE_HINT) && SDK_STORE_HINT == 1
   __builtin_nontemporal_store(v, reinterpret_cast<h8*>(p));
+#elif defined(SDK_STORE_HINT) && SDK_STORE_HINT == 2
+  asm volatile("" ::"v"(v), "v"(p));   // A/B build only: the whole epilogue but its global stores
 #else
   *reinterpret_cast<h8*>(p) = v;
 #endif
@@ -670,7 +683,7 @@ __device__ __forceinline__ void epilogue_lds(const Params& p, f16v (&acc)[FM][FN
         for (int g = 0; g < 4; ++g) {
           const int nx = n0 + n_w + jp * 64 + 8 * g + 4 * fh;
           f4 bx = {0.f, 0.f, 0.f, 0.f}, bg = {0.f, 0.f, 0.f, 0.f};
-          if (p.bias) {
+          if (bias_s || p.bias) {
             bx = bias4(nx);
             bg = bias4(nx + 32);
           }
@@ -749,7 +762,12 @@ __device__ __forceinline__ void epilogue_lds(const Params& p, f16v (&acc)[FM][FN
           float v[4];
 #pragma unroll
           for (int qq = 0; qq < 4; ++qq) v[qq] = acc[i][jp + jj][4 * g + qq];
-          if (n < p.N) {                          // N % 8 == 0 in this mode
+          if (rb_s) {                             // staged vectors (zeros where absent): branch-free
+            const f4 bb = *reinterpret_cast<const f4*>(bias_s + (n - n0));
+            const f4 r4 = *reinterpret_cast<const f4*>(rb_s + (n - n0));
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq) v[qq] = (v[qq] + bb[qq]) + r4[qq];
+          } else if (n < p.N) {                   // N % 8 == 0 in this mode
             if (p.bias) {
               const f4 bb = bias4(n);
 #pragma unroll
@@ -848,7 +866,7 @@ __device__ __forceinline__ void epi16_group(const Params& p, const f4* a, int mt
     for (int j = 0; j < 2; ++j) {
       const int nx = nb + 16 * j + 4 * cg;
       f4 bx = {0.f, 0.f, 0.f, 0.f}, bg = {0.f, 0.f, 0.f, 0.f};
-      if (p.bias) {
+      if (bias_s || p.bias) {
         bx = bias4(nx);
         bg = bias4(nx + 32);
       }
@@ -870,6 +888,20 @@ __device__ __forceinline__ void epi16_group(const Params& p, const f4* a, int mt
     return;
   }
   if (nb >= p.N) return;
+  if (rb_s) {
+    // staged bias and embedding row (zeros where absent or past N; the read-back masks columns >= N):
+    // the same two adds in the same order as below, no per-chunk branches
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int off = nb - n0 + 16 * j + 4 * cg;
+      const f4 bb = *reinterpret_cast<const f4*>(bias_s + off);
+      const f4 r4 = *reinterpret_cast<const f4*>(rb_s + off);
+      h4 o;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = (half_t)((a[j][q] + bb[q]) + r4[q]);
+      *reinterpret_cast<h4*>(wbuf + px * EPG_RS + 16 * j + 4 * cg) = o;
+    }
+  } else
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
     const int n = nb + 16 * j + 4 * cg;
@@ -956,6 +988,7 @@ __device__ __forceinline__ void epilogue16_tile(const Params& p, f4 (&acc)[FM][F
         epi16_group<2, GN>(p, &acc[i][FN - 2], mt, n0 + n_w + 16 * (FN - 2), n0, bw, rb_vec, wbuf, bias_s, rb_s,
                            rcur, gst + i * TN + 64 * g);
     }
+    if (q < 4) ph_stamp(p, 4 + q);
     if (p.res && AHEAD && q + 1 < NQ) {
       rcur[0] = rnext[0];
       rcur[1] = rnext[1];
@@ -1243,6 +1276,7 @@ __global__ void __launch_bounds__(CF::NT, CF::OCC * CF::NW / 4) conv_glds_kernel
   const int it = xcd_remap((int)blockIdx.x + (int)blockIdx.y * (int)gridDim.x, nitems);
   int tm, tn, sidx;
   item_coords(p, it, tm, tn, sidx);
+  ph_stamp(p, 0);
   const int m0 = tm * CF::TBM, n0 = tn * CF::TBN;
   const int kt0 = sidx * p.kt_per_split, kt1 = min(p.kt_total, kt0 + p.kt_per_split);
   const int lrow = lane >> 3;
@@ -1318,6 +1352,7 @@ __global__ void __launch_bounds__(CF::NT, CF::OCC * CF::NW / 4) conv_glds_kernel
   // each K-step's MFMA cluster measured +0.2 %)
   if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= CF::NT / 2) __builtin_amdgcn_s_setprio(1);
 #endif
+  ph_stamp(p, 1);
   for (int kt = kt0; kt < kt1; ++kt) {
     SDK_STAGE(kt + CF::NS - 1, wbuf);
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"((CF::NS - 1) * GPW) : "memory");
@@ -1367,6 +1402,7 @@ __global__ void __launch_bounds__(CF::NT, CF::OCC * CF::NW / 4) conv_glds_kernel
 #undef SDK_STAGE
   // the trailing zero-page DMAs land before the ring is reused as epilogue scratch
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  ph_stamp(p, 2);
   if (p.inl) {
     // in-launch split-K: both halves dump their accumulators as a lane-major blob (16-B stores, every wave
     // instruction a contiguous KiB), publish with an agent-scope release and take a ticket; the second
@@ -1434,8 +1470,10 @@ __global__ void __launch_bounds__(CF::NT, CF::OCC * CF::NW / 4) conv_glds_kernel
   float* vec_s = reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + CF::RING_BYTES);
   epi_vec_store(ev, vec_s, CF::TBN);
   __builtin_amdgcn_s_barrier();
-  const float* bias_s = p.bias ? vec_s : nullptr;
-  const float* rb_s = ev.one_img ? vec_s + CF::TBN : nullptr;
+  // the staged vectors hold zeros where there is no bias / embedding row; rb_s = nullptr only where the
+  // tile's rows span two images' embedding rows (the epilogue then reads them per row from global)
+  const float* bias_s = vec_s;
+  const float* rb_s = (ev.one_img || !p.row_bias) ? vec_s + CF::TBN : nullptr;
   constexpr int WSCR = CF::RING_BYTES / CF::NW / 16 * 8;   // per-wave epilogue scratch (halfs)
   half_t* wscr = lds + wave * WSCR;
   const bool lds_epi = (p.split == 1 || p.inl) && (p.out_mode == SDK_OUT_NHWC_F16 || p.out_mode == SDK_OUT_GEGLU_F16);
@@ -1455,6 +1493,7 @@ __global__ void __launch_bounds__(CF::NT, CF::OCC * CF::NW / 4) conv_glds_kernel
     } else {
       epilogue16_tile_direct<CF::FM16, CF::FN16>(p, acc16, m0, n0, wm * CF::TM, wn * CF::TN, sidx);
     }
+    ph_stamp(p, 3);
     return;
   }
   if (lds_epi && p.gnp) {
@@ -1465,6 +1504,7 @@ __global__ void __launch_bounds__(CF::NT, CF::OCC * CF::NW / 4) conv_glds_kernel
   } else {
     epilogue_direct<CF::FM, CF::FN>(p, acc, m0, n0, wm * CF::TM, wn * CF::TN, sidx);
   }
+  ph_stamp(p, 3);
 }
 
 using Cfg256x256 = Cfg<256, 256, 2, 4>;
@@ -1809,8 +1849,10 @@ __global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_halo_kernel(Params p)
   float* vec_s = reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + CF::WRING_BYTES + RP * 1024);
   epi_vec_store(ev, vec_s, CF::TBN);
   __builtin_amdgcn_s_barrier();
-  const float* bias_s = p.bias ? vec_s : nullptr;
-  const float* rb_s = ev.one_img ? vec_s + CF::TBN : nullptr;
+  // the staged vectors hold zeros where there is no bias / embedding row; rb_s = nullptr only where the
+  // tile's rows span two images' embedding rows (the epilogue then reads them per row from global)
+  const float* bias_s = vec_s;
+  const float* rb_s = (ev.one_img || !p.row_bias) ? vec_s + CF::TBN : nullptr;
   constexpr int WSCR = CF::WRING_BYTES / CF::NW / 16 * 8;   // per-wave epilogue scratch (halfs) in the W ring
   half_t* wscr = lds + wave * WSCR;
   const bool lds_epi = p.split == 1 && p.out_mode == SDK_OUT_NHWC_F16;
@@ -1836,7 +1878,8 @@ constexpr int EPI16_RS = 72;                          // scratch row stride (hal
 constexpr int EPI16_BYTES = 16 * EPI16_RS * 2;        // per-wave scratch: 16 pixels x 64 channels
 
 __device__ __forceinline__ void epilogue16_lds(const Params& p, f4 (&acc)[4][2][2], int m0, int n0, int m_w, int n_w,
-                                               half_t* wbuf) {
+                                               half_t* wbuf, const float* bias_s = nullptr,
+                                               const float* rb_s = nullptr) {
   const int lane = threadIdx.x & 63, px = lane & 15, cg = lane >> 4;
   const bool rb_vec = p.row_bias && !((uintptr_t)p.row_bias & 15) && !(p.rb_ld & 3);
   half_t* out = reinterpret_cast<half_t*>(p.out);
@@ -1852,7 +1895,10 @@ __device__ __forceinline__ void epilogue16_lds(const Params& p, f4 (&acc)[4][2][
       for (int j = 0; j < 2; ++j) {
         const int nx = n0 + n_w + 16 * j + 4 * cg;    // x rows; gate rows = nx + 32
         f4 bx = {0.f, 0.f, 0.f, 0.f}, bg = {0.f, 0.f, 0.f, 0.f};
-        if (p.bias) {
+        if (bias_s) {                                 // staged (zeros where there is no bias)
+          bx = *reinterpret_cast<const f4*>(bias_s + (nx - n0));
+          bg = *reinterpret_cast<const f4*>(bias_s + (nx + 32 - n0));
+        } else if (p.bias) {
           bx = *reinterpret_cast<const f4*>(p.bias + nx);
           bg = *reinterpret_cast<const f4*>(p.bias + nx + 32);
         }
@@ -1884,7 +1930,12 @@ __device__ __forceinline__ void epilogue16_lds(const Params& p, f4 (&acc)[4][2][
         float v[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = acc[i][b][j][q];
-        if (n < p.N) {                                // N % 8 == 0 in this mode
+        if (rb_s) {                                   // staged vectors (zeros where absent): branch-free
+          const f4 bb = *reinterpret_cast<const f4*>(bias_s + (n - n0));
+          const f4 r4 = *reinterpret_cast<const f4*>(rb_s + (n - n0));
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = (v[q] + bb[q]) + r4[q];
+        } else if (n < p.N) {                         // N % 8 == 0 in this mode
           if (p.bias) {
             const f4 bb = *reinterpret_cast<const f4*>(p.bias + n);
 #pragma unroll
@@ -1997,6 +2048,7 @@ __global__ void __launch_bounds__(512) conv_ph_kernel(Params p) {
   const int nitems = p.tiles_m * p.tiles_n * p.split;
   const int it = xcd_remap((int)blockIdx.x + (int)blockIdx.y * (int)gridDim.x, nitems);
   int tm, tn, sidx;
+  ph_stamp(p, 0);
   item_coords(p, it, tm, tn, sidx);
   const int m0 = tm * 256, n0 = tn * 256;
   const int kt0 = sidx * p.kt_per_split, kt1 = min(p.kt_total, kt0 + p.kt_per_split);
@@ -2084,6 +2136,7 @@ __global__ void __launch_bounds__(512) conv_ph_kernel(Params p) {
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
+  ph_stamp(p, 1);
 
   f16v acc[2][2][2];   // [A half][pixel tile][W half]                      (32x32x16 path)
   f4 acc16[2][4][2][2];   // [A half][16-pixel block][W half][16-channel block] (16x16x32 path)
@@ -2193,6 +2246,7 @@ __global__ void __launch_bounds__(512) conv_ph_kernel(Params p) {
   }
   if (wr == 0) SDK_PH_BAR();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  ph_stamp(p, 2);
 #undef SDK_PH_BAR
 #undef SDK_PH_ISSUE
 #undef SDK_PH_ISSUE_A
@@ -2216,12 +2270,13 @@ __global__ void __launch_bounds__(512) conv_ph_kernel(Params p) {
   float* vec_s = reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + PC::RING_BYTES);
   if constexpr (PC::VEC) epi_vec_store(ev, vec_s, 256);
   __builtin_amdgcn_s_barrier();
-  const float* bias_s = (PC::VEC && p.bias) ? vec_s : nullptr;
-  const float* rb_s = (PC::VEC && ev.one_img) ? vec_s + 256 : nullptr;
+  const float* bias_s = PC::VEC ? vec_s : nullptr;   // zeros where absent (as in conv_glds_kernel)
+  const float* rb_s = (PC::VEC && (ev.one_img || !p.row_bias)) ? vec_s + 256 : nullptr;
   if constexpr (M16) {
     if (p.split == 1 && (p.out_mode == SDK_OUT_NHWC_F16 || p.out_mode == SDK_OUT_GEGLU_F16)) {
-      epilogue16_lds(p, acc16[0], m0, n0, wr * 64, wc * 64, lds + wave * (EPI16_BYTES / 2));
-      epilogue16_lds(p, acc16[1], m0, n0, 128 + wr * 64, wc * 64, lds + wave * (EPI16_BYTES / 2));
+      epilogue16_lds(p, acc16[0], m0, n0, wr * 64, wc * 64, lds + wave * (EPI16_BYTES / 2), bias_s, rb_s);
+      epilogue16_lds(p, acc16[1], m0, n0, 128 + wr * 64, wc * 64, lds + wave * (EPI16_BYTES / 2), bias_s, rb_s);
+      ph_stamp(p, 3);
     } else {
       epilogue16_direct(p, acc16[0], m0, n0, wr * 64, wc * 64, sidx);
       epilogue16_direct(p, acc16[1], m0, n0, 128 + wr * 64, wc * 64, sidx);
@@ -2247,6 +2302,7 @@ __global__ void __launch_bounds__(512) conv_ph_kernel(Params p) {
     }
     epilogue_lds<2, 2>(p, acc[0], m0, n0, wr * 64, wc * 64, lds + wave * (EPI_BYTES / 2), bias_s, rb_s);
     epilogue_lds<2, 2>(p, acc[1], m0, n0, 128 + wr * 64, wc * 64, lds + wave * (EPI_BYTES / 2), bias_s, rb_s);
+    ph_stamp(p, 3);
   } else {
     epilogue_direct<2, 2>(p, acc[0], m0, n0, wr * 64, wc * 64, sidx);
     epilogue_direct<2, 2>(p, acc[1], m0, n0, 128 + wr * 64, wc * 64, sidx);
@@ -2664,6 +2720,8 @@ int launch_halo(const Params& p, hipStream_t s) {
 }
 
 #ifdef SDK_CONV_DIAGNOSTICS
+unsigned long long* g_conv_stamps = nullptr;   // 8 stamps x 65536 workgroups (SDK_CONV_STAMPS=1)
+constexpr int kStampWgs = 65536;
 constexpr bool kDiagnostics = true;
 #else
 constexpr bool kDiagnostics = false;
@@ -2920,6 +2978,13 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
       split = (kt + p.kt_per_split - 1) / p.kt_per_split;
       p.split = split;
       p.gm = split == 1 ? tile_group_m(a, p) : 1;
+#ifdef SDK_CONV_DIAGNOSTICS
+  if (getenv("SDK_CONV_STAMPS")) {
+    if (!g_conv_stamps && (hipMalloc((void**)&g_conv_stamps, (size_t)kStampWgs * 8 * 8) != hipSuccess ||
+                           hipMemset(g_conv_stamps, 0, (size_t)kStampWgs * 8 * 8) != hipSuccess)) g_conv_stamps = nullptr;
+    if ((long long)p.tiles_m * p.tiles_n * p.split <= kStampWgs) p.stamps = g_conv_stamps;
+  }
+#endif
       const int64_t ws = split > 1 ? (int64_t)split * p.M * p.Npad * 4 : 0;
       int gn_nch = 0;
       if (a->out_mode == SDK_OUT_NHWC_F16) {
@@ -3005,6 +3070,13 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   split = (kt + p.kt_per_split - 1) / p.kt_per_split;
   p.split = split;
   p.gm = split == 1 ? tile_group_m(a, p) : 1;
+#ifdef SDK_CONV_DIAGNOSTICS
+  if (getenv("SDK_CONV_STAMPS")) {
+    if (!g_conv_stamps && (hipMalloc((void**)&g_conv_stamps, (size_t)kStampWgs * 8 * 8) != hipSuccess ||
+                           hipMemset(g_conv_stamps, 0, (size_t)kStampWgs * 8 * 8) != hipSuccess)) g_conv_stamps = nullptr;
+    if ((long long)p.tiles_m * p.tiles_n * p.split <= kStampWgs) p.stamps = g_conv_stamps;
+  }
+#endif
   int64_t ws = split > 1 ? (int64_t)split * p.M * p.Npad * 4 : 0;
   if (a->split_inlaunch) {
     const bool tile_kernel = (var >= 2 && var <= 7) || (var >= 16 && var <= 19) || (var >= 22 && var <= 26) ||
@@ -3126,3 +3198,11 @@ extern "C" int sdk_conv2d(const sdk_conv_args* a, sdk_stream_t stream) {
   }
   return SDK_OK;
 }
+
+#ifdef SDK_CONV_DIAGNOSTICS
+// diagnostics build only (not in include/sdk_amd.h): copy the phase stamps of the last stamped launches
+extern "C" int sdk_diag_conv_stamps(unsigned long long* host, long long n) {
+  if (!g_conv_stamps || n <= 0 || n > (long long)kStampWgs * 8) return SDK_EINVAL;
+  return hipMemcpy(host, g_conv_stamps, (size_t)n * 8, hipMemcpyDeviceToHost) == hipSuccess ? SDK_OK : SDK_EINVAL;
+}
+#endif

@@ -233,6 +233,8 @@ class _Autotune:
     VARIANTS = (2, 5, 7, 6, 4, 3, 8, 9, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 31, 32, 33, 34, 35, 36, 37)
     # split -2: two K halves combined inside the launch (sdk_conv_args.split_inlaunch; LDS-DMA tile kernels)
     SPLITS = (0, 1, 2, 4, 8, -2)
+    # unsplit plans: M-panels per tile group (sdk_conv_args.tile_group_m; 1 = M-panel major)
+    GROUPS = (1, 8, 16)
 
     def __init__(self):
         import os
@@ -248,7 +250,7 @@ class _Autotune:
         self.enabled = on
 
     def save(self, path):
-        """Write the table as JSON (key tuple -> [variant_hint, split_k]); a tuning cache
+        """Write the table as JSON (key tuple -> [variant_hint, split_k, tile_group_m]); a tuning cache
         like MIOpen's find-db: later runs load it and time nothing."""
         import json
         with open(path, "w") as f:
@@ -322,17 +324,19 @@ class _Autotune:
                 if info.workspace_bytes > 0:
                     ws = WORKSPACE.get(info.workspace_bytes, dev)
                     a.workspace, a.workspace_bytes = ws.data_ptr(), ws.numel()
-                check(lib().sdk_conv2d(C.byref(a), stream), "conv2d(autotune)")
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                for _ in range(self.reps):
-                    lib().sdk_conv2d(C.byref(a), stream)
-                e1.record()
-                e1.synchronize()
-                t = e0.elapsed_time(e1)
-                if t < best_t:
-                    best_t, best = t, (v + 1, -2 if sp == -2 else info.split_k)
-        a.variant_hint, a.gn_partial = 0, None
+                for gm in (self.GROUPS if info.split_k == 1 else (0,)):
+                    a.tile_group_m = gm
+                    check(lib().sdk_conv2d(C.byref(a), stream), "conv2d(autotune)")
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for _ in range(self.reps):
+                        lib().sdk_conv2d(C.byref(a), stream)
+                    e1.record()
+                    e1.synchronize()
+                    t = e0.elapsed_time(e1)
+                    if t < best_t:
+                        best_t, best = t, (v + 1, -2 if sp == -2 else info.split_k, gm)
+        a.variant_hint, a.gn_partial, a.tile_group_m = 0, None, 0
         set_split(a, 0, dev)
         self.table[key] = best
         self.timed += 1
@@ -493,6 +497,7 @@ def conv2d(pc: PackedConv, x, *, ksize=None, stride=1, pad=None, pad_end=0, upsa
     if tuned is not None:
         a.variant_hint = tuned[0]
         set_split(a, tuned[1], dev)
+        a.tile_group_m = tuned[2] if len(tuned) > 2 else 0
     if variant is None:
         variant = FORCE_VARIANT
     if variant is not None:

@@ -1,5 +1,5 @@
 """Time one conv configuration (for rocprofv3 counter passes and A/B runs).
-usage: python tools/conv_probe.py <shape> <variant> <split> [iters]
+usage: [GM=<tile_group_m>] python tools/conv_probe.py <shape> <variant> <split> [iters]
 shape: a tools/bench_conv.py SHAPES name, or B,H,W,Cin,Cout,k,up"""
 import os, sys
 import torch
@@ -11,6 +11,8 @@ def main():
     import sd_amd_loader
     sd_amd_loader.load()
     from sd_amd import ops
+    if os.environ.get("GM"):          # tile group (sdk_conv_args.tile_group_m)
+        ops.TILE_GROUP_M = int(os.environ["GM"])
     name, variant, split = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
     iters = int(sys.argv[4]) if len(sys.argv) > 4 else 20
     spec = {s[0]: s[1:] for s in SHAPES}.get(name)
