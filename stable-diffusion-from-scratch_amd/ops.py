@@ -501,6 +501,11 @@ def conv2d(pc: PackedConv, x, *, ksize=None, stride=1, pad=None, pad_end=0, upsa
     if variant is None:
         variant = FORCE_VARIANT
     if variant is not None:
+        if variant + 1 != a.variant_hint:
+            # a forced configuration: the tuned split / tile order belong to the tuned variant (an in-launch
+            # split may not even exist for this one) -> the planner's split for the forced variant
+            set_split(a, 0, dev)
+            a.tile_group_m = 0
         a.variant_hint = variant + 1
     if split_k is not None:
         set_split(a, split_k, dev)    # -2: the in-launch combine of two K halves
