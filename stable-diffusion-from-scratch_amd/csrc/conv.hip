@@ -83,6 +83,7 @@ struct Params {
   unsigned* tcnt;
   int gm;               // unsplit plans: tiles visited in groups of gm M-panels, N-tile major inside a group
   unsigned long long* stamps;   // diagnostics build only: 8 shader-clock stamps per workgroup, or null
+  int simple;           // token GEMM (one segment, 1x1 stride 1, no masks, one source): linear A / W K offsets
 };
 
 // diagnostics build: s_memtime at kernel entry / after the prologue / after the K loop / at the end (+ after
@@ -1264,7 +1265,12 @@ __device__ __forceinline__ void item_coords(const Params& p, int it, int& tm, in
 }
 
 // One (tile, K-split) work item per workgroup, two LDS stages.
-template <class CF>
+// SIMPLE: the instantiation for one-segment, one-source convs without masks (build_params sets p.simple:
+// token GEMMs and the 3x3 convs over zero-bordered inputs): a lane's A row offset is fixed (the tap window's
+// origin pixel) and a K step adds one wave-uniform offset (tap + channel block), so an A piece is one DMA
+// with that offset in the scalar soffset like a W piece — no per-piece segment / tap / mask branch chains in
+// the K loop (their scalar work bounded the loop: +19-28 % on the UNet token GEMMs).
+template <class CF, bool SIMPLE = false>
 __global__ void __launch_bounds__(CF::NT, CF::OCC * CF::NW / 4) conv_glds_kernel(Params p) {
   extern __shared__ __attribute__((aligned(16))) half_t lds[];
   constexpr int GPW = CF::GPW;
@@ -1289,8 +1295,16 @@ __global__ void __launch_bounds__(CF::NT, CF::OCC * CF::NW / 4) conv_glds_kernel
     const int rch = (lane & 7) ^ ((4 * piece + (lrow >> 1)) & 7);
     unsigned x = PH_OOB, y = 0;
     if (piece < CF::NINSTR) {
-      if (piece * 8 < CF::TBM) a_row_ctx(p, m0 + piece * 8 + lrow, x, y);
-      else x = w_row_ctx(p, n0 + piece * 8 + lrow - CF::TBM, rch);
+      if (piece * 8 < CF::TBM) {
+        if constexpr (SIMPLE) {   // the tap window origin's row, 16-B chunk rch of the K step
+          a_row_ctx(p, m0 + piece * 8 + lrow, x, y);
+          x = (m0 + piece * 8 + lrow) < p.M ? __umul24(x, (unsigned)p.seg[0].ld0 * 2u) + (unsigned)rch * 16u : PH_OOB;
+        } else {
+          a_row_ctx(p, m0 + piece * 8 + lrow, x, y);
+        }
+      } else {
+        x = w_row_ctx(p, n0 + piece * 8 + lrow - CF::TBM, rch);
+      }
     }
     cx[j] = x;
     cy[j] = y;
@@ -1303,6 +1317,21 @@ __global__ void __launch_bounds__(CF::NT, CF::OCC * CF::NW / 4) conv_glds_kernel
 #define SDK_STAGE(KT_, BUF_)                                                                 \
   do {                                                                                       \
     const bool live_ = (KT_) < kt1;                                                          \
+    if constexpr (SIMPLE) {                                                                  \
+      const int toff_ = (ky * p.seg[0].w + kx) * p.seg[0].ld0 * 2 + cb * 2;                  \
+      _Pragma("unroll") for (int j = 0; j < GPW; ++j) {                                      \
+        const int piece = j * CF::NW + wave;                                                 \
+        if (piece >= CF::NINSTR) {                                                           \
+          ph_dma(d.w, lds + CF::NS * CF::STAGE_H, PH_OOB, 0);                                \
+        } else {                                                                             \
+          const bool a_ = piece * 8 < CF::TBM;                                               \
+          ph_dma(a_ ? d.a0 : d.w, lds + (BUF_) * CF::STAGE_H + piece * 8 * BK,               \
+                 live_ ? cx[j] : PH_OOB, a_ ? toff_ : (KT_) * BK * 2);                       \
+        }                                                                                    \
+      }                                                                                      \
+      if (live_) ph_kadv(p, sg, ky, kx, cb);                                                 \
+      break;                                                                                 \
+    }                                                                                        \
     _Pragma("unroll") for (int j = 0; j < GPW; ++j) {                                        \
       const int piece = j * CF::NW + wave;                                                   \
       const int rch = (lane & 7) ^ ((4 * piece + (lrow >> 1)) & 7);                          \
@@ -2038,7 +2067,9 @@ struct PhCfg {
 };
 constexpr int PH_HALF = 128 * BK;   // halfs per half-tile slot
 
-template <class PC, int DBG = 0, bool M16 = false>
+// SIMPLE (p.simple, DBG == 0): the linear A issue of conv_glds_kernel — per-lane row offsets fixed, the K step's
+// tap / channel offset in the scalar soffset
+template <class PC, int DBG = 0, bool M16 = false, bool SIMPLE = false>
 __global__ void __launch_bounds__(512) conv_ph_kernel(Params p) {
   extern __shared__ __attribute__((aligned(16))) half_t lds[];
   constexpr int S = PC::S, D = PC::D;
@@ -2065,6 +2096,9 @@ __global__ void __launch_bounds__(512) conv_ph_kernel(Params p) {
   for (int q = 0; q < 4; ++q) {
     const int a = q >> 1, j = q & 1;
     a_row_ctx(p, mrow + a * 128 + j * 64, pixb[q], msk[q]);
+    if constexpr (SIMPLE)   // pixb -> the lane's byte offset (tap window origin, chunk rch), or out of range
+      pixb[q] = mrow + a * 128 + j * 64 < p.M ? __umul24(pixb[q], (unsigned)p.seg[0].ld0 * 2u) + (unsigned)rch * 16u
+                                              : PH_OOB;
     const int pc = j * 8 + wave;
     wv[q] = w_row_ctx(p, n0 + 64 * (pc >> 2) + 32 * a + 8 * (pc & 3) + lrow, rch);
   }
@@ -2073,7 +2107,11 @@ __global__ void __launch_bounds__(512) conv_ph_kernel(Params p) {
   do {                                                                                     \
     half_t* sl_ = lds + (SLOT) * PH_HALF + wave * 8 * BK;                                  \
     const int kt_ = kt0 + (T);                                                             \
-    if (DBG & (1 | 256)) {                                                                 \
+    if constexpr (SIMPLE && DBG == 0) {                                                    \
+      const int toff_ = ((KY) * p.seg[0].w + (KX)) * p.seg[0].ld0 * 2 + (CB) * 2;          \
+      _Pragma("unroll") for (int j = 0; j < 2; ++j)                                        \
+        ph_dma(d.a0, sl_ + j * 64 * BK, kt_ < kt1 ? pixb[(A_) * 2 + j] : PH_OOB, toff_);    \
+    } else if (DBG & (1 | 256)) {                                                          \
     } else if (kt_ >= kt1) {                                                               \
       _Pragma("unroll") for (int j = 0; j < 2; ++j) ph_dma(d.w, sl_ + j * 64 * BK, PH_OOB, 0); \
     } else if (DBG & 512) {                                                                \
@@ -2314,7 +2352,16 @@ using PhCfg10 = PhCfg<10, 8>;
 
 template <class PC, int DBG = 0, bool M16 = false>
 int launch_ph(const Params& p, hipStream_t s) {
-  static std::atomic<unsigned long long> attr_set{0};
+  static std::atomic<unsigned long long> attr_set{0}, attr_simple{0};
+  if constexpr (DBG == 0) {
+    if (p.simple) {
+      if (int e = ensure_dyn_lds((const void*)conv_ph_kernel<PC, 0, M16, true>, PC::LDS_BYTES, attr_simple, "conv2d"))
+        return e;
+      hipLaunchKernelGGL((conv_ph_kernel<PC, 0, M16, true>), dim3(p.tiles_m * p.tiles_n, p.split), dim3(512),
+                         PC::LDS_BYTES, s, p);
+      return check_launch("conv_ph");
+    }
+  }
   if (int e = ensure_dyn_lds((const void*)conv_ph_kernel<PC, DBG, M16>, PC::LDS_BYTES, attr_set, "conv2d")) return e;
   hipLaunchKernelGGL((conv_ph_kernel<PC, DBG, M16>), dim3(p.tiles_m * p.tiles_n, p.split), dim3(512),
                      PC::LDS_BYTES, s, p);
@@ -2691,7 +2738,13 @@ int launch_skinny(const Params& p, hipStream_t s) {
 
 template <class CF>
 int launch_glds(const Params& p, hipStream_t s) {
-  static std::atomic<unsigned long long> attr_set{0};   // per device: the dynamic-LDS cap is raised once
+  static std::atomic<unsigned long long> attr_set{0}, attr_simple{0};   // per device: the dynamic-LDS cap, once
+  if (p.simple) {
+    if (int e = ensure_dyn_lds((const void*)conv_glds_kernel<CF, true>, CF::LDS_BYTES, attr_simple, "conv2d")) return e;
+    hipLaunchKernelGGL((conv_glds_kernel<CF, true>), dim3(p.tiles_m * p.tiles_n, p.split), dim3(CF::NT), CF::LDS_BYTES,
+                       s, p);
+    return check_launch("conv_glds");
+  }
   if (int e = ensure_dyn_lds((const void*)conv_glds_kernel<CF>, CF::LDS_BYTES, attr_set, "conv2d")) return e;
   hipLaunchKernelGGL((conv_glds_kernel<CF>), dim3(p.tiles_m * p.tiles_n, p.split), dim3(CF::NT), CF::LDS_BYTES, s,
                      p);
@@ -2791,6 +2844,8 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
     const sdk_conv_src& g = a->seg[0];
     p.nomask = g.pad == 0 && g.pad_end == 0 && !g.upsample && g.cin % BK == 0 &&
                (g.c_split == g.cin || g.c_split % BK == 0) && g.gn_scale == nullptr && !g.silu;
+    // the linear K loop of the LDS-DMA kernels (conv_glds_kernel SIMPLE): one segment, one source, no masks
+    p.simple = p.nomask && a->nseg == 1 && (!g.src1 || g.c_split >= g.cin);
   }
   if (a->out_mode == SDK_OUT_NHWC_F16 || a->out_mode == SDK_OUT_GEGLU_F16) {
     if (a->cout % 8 || a->out_ld % 8 || (a->residual && a->res_ld % 8))

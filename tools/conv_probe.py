@@ -25,7 +25,8 @@ def main():
     x = torch.randn(B, H, W, Ci, device="cuda").half()
     w = torch.randn(Co, Ci, k, k, device="cuda") / (Ci * k * k) ** 0.5
     pc = ops.PackedConv([(w, Ci)], torch.zeros(Co, device="cuda"), geglu=bool(geglu), device="cuda")
-    kw = dict(stride=st, pad=k // 2, upsample=bool(up), variant=None if variant < 0 else variant,
+    kw = dict(stride=st, pad=0 if name.endswith("_prepad") else k // 2, upsample=bool(up),
+              variant=None if variant < 0 else variant,
               split_k=None if split <= 0 else split,
               out_mode=ops.OUT_GEGLU_F16 if geglu else ops.OUT_NHWC_F16)
     y = ops.conv2d(pc, x, **kw)
