@@ -1270,7 +1270,9 @@ __device__ __forceinline__ void item_coords(const Params& p, int it, int& tm, in
 // origin pixel) and a K step adds one wave-uniform offset (tap + channel block), so an A piece is one DMA
 // with that offset in the scalar soffset like a W piece — no per-piece segment / tap / mask branch chains in
 // the K loop (their scalar work bounded the loop: +19-28 % on the UNet token GEMMs).
-template <class CF, bool SIMPLE = false>
+// SIMPLE = 2: the same with a second, 1x1 segment over the output grid (a ResBlock's fused shortcut, one or two
+// concat sources): the K step's segment / source picks one of three per-lane row offsets.
+template <class CF, int SIMPLE = 0>
 __global__ void __launch_bounds__(CF::NT, CF::OCC * CF::NW / 4) conv_glds_kernel(Params p) {
   extern __shared__ __attribute__((aligned(16))) half_t lds[];
   constexpr int GPW = CF::GPW;
@@ -1288,7 +1290,7 @@ __global__ void __launch_bounds__(CF::NT, CF::OCC * CF::NW / 4) conv_glds_kernel
   const int lrow = lane >> 3;
   const DmaSrc d = make_dma_src(p, m0);
   // per piece j (rows (j*NW + wave)*8 + lrow of the stage): A -> (pixb, msk), W -> byte offset
-  unsigned cx[GPW], cy[GPW];
+  unsigned cx[GPW], cy[GPW], cz[SIMPLE == 2 ? GPW : 1];
 #pragma unroll
   for (int j = 0; j < GPW; ++j) {
     const int piece = j * CF::NW + wave;
@@ -1296,9 +1298,14 @@ __global__ void __launch_bounds__(CF::NT, CF::OCC * CF::NW / 4) conv_glds_kernel
     unsigned x = PH_OOB, y = 0;
     if (piece < CF::NINSTR) {
       if (piece * 8 < CF::TBM) {
-        if constexpr (SIMPLE) {   // the tap window origin's row, 16-B chunk rch of the K step
-          a_row_ctx(p, m0 + piece * 8 + lrow, x, y);
-          x = (m0 + piece * 8 + lrow) < p.M ? __umul24(x, (unsigned)p.seg[0].ld0 * 2u) + (unsigned)rch * 16u : PH_OOB;
+        if constexpr (SIMPLE != 0) {   // the tap window origin's row, 16-B chunk rch of the K step
+          const int m = m0 + piece * 8 + lrow;
+          a_row_ctx(p, m, x, y);
+          x = m < p.M ? __umul24(x, (unsigned)p.seg[0].ld0 * 2u) + (unsigned)rch * 16u : PH_OOB;
+          if constexpr (SIMPLE == 2) {   // the shortcut segment: output pixel m of each concat source
+            y = m < p.M ? __umul24((unsigned)m, (unsigned)p.seg[1].ld0 * 2u) + (unsigned)rch * 16u : PH_OOB;
+            cz[j] = m < p.M ? __umul24((unsigned)m, (unsigned)p.seg[1].ld1 * 2u) + (unsigned)rch * 16u : PH_OOB;
+          }
         } else {
           a_row_ctx(p, m0 + piece * 8 + lrow, x, y);
         }
@@ -1317,16 +1324,28 @@ __global__ void __launch_bounds__(CF::NT, CF::OCC * CF::NW / 4) conv_glds_kernel
 #define SDK_STAGE(KT_, BUF_)                                                                 \
   do {                                                                                       \
     const bool live_ = (KT_) < kt1;                                                          \
-    if constexpr (SIMPLE) {                                                                  \
-      const int toff_ = (ky * p.seg[0].w + kx) * p.seg[0].ld0 * 2 + cb * 2;                  \
+    if constexpr (SIMPLE != 0) {                                                             \
+      int toff_ = (ky * p.seg[0].w + kx) * p.seg[0].ld0 * 2 + cb * 2;                        \
+      __amdgpu_buffer_rsrc_t ra_ = d.a0;                                                     \
+      bool s1_ = false, sec_ = false;                                                        \
+      if constexpr (SIMPLE == 2) {                                                           \
+        s1_ = sg != 0;                                                                       \
+        sec_ = s1_ && cb >= p.seg[1].c_split;                                                \
+        if (s1_) {                                                                           \
+          toff_ = (cb - (sec_ ? p.seg[1].c_split : 0)) * 2;                                  \
+          ra_ = sec_ ? d.s1 : d.s0;                                                          \
+        }                                                                                    \
+      }                                                                                      \
       _Pragma("unroll") for (int j = 0; j < GPW; ++j) {                                      \
         const int piece = j * CF::NW + wave;                                                 \
         if (piece >= CF::NINSTR) {                                                           \
           ph_dma(d.w, lds + CF::NS * CF::STAGE_H, PH_OOB, 0);                                \
         } else {                                                                             \
           const bool a_ = piece * 8 < CF::TBM;                                               \
-          ph_dma(a_ ? d.a0 : d.w, lds + (BUF_) * CF::STAGE_H + piece * 8 * BK,               \
-                 live_ ? cx[j] : PH_OOB, a_ ? toff_ : (KT_) * BK * 2);                       \
+          unsigned base_ = cx[j];                                                            \
+          if constexpr (SIMPLE == 2) base_ = (a_ && s1_) ? (sec_ ? cz[j] : cy[j]) : cx[j];   \
+          ph_dma(a_ ? ra_ : d.w, lds + (BUF_) * CF::STAGE_H + piece * 8 * BK,                \
+                 live_ ? base_ : PH_OOB, a_ ? toff_ : (KT_) * BK * 2);                       \
         }                                                                                    \
       }                                                                                      \
       if (live_) ph_kadv(p, sg, ky, kx, cb);                                                 \
@@ -2354,7 +2373,7 @@ template <class PC, int DBG = 0, bool M16 = false>
 int launch_ph(const Params& p, hipStream_t s) {
   static std::atomic<unsigned long long> attr_set{0}, attr_simple{0};
   if constexpr (DBG == 0) {
-    if (p.simple) {
+    if (p.simple == 1) {
       if (int e = ensure_dyn_lds((const void*)conv_ph_kernel<PC, 0, M16, true>, PC::LDS_BYTES, attr_simple, "conv2d"))
         return e;
       hipLaunchKernelGGL((conv_ph_kernel<PC, 0, M16, true>), dim3(p.tiles_m * p.tiles_n, p.split), dim3(512),
@@ -2739,9 +2758,16 @@ int launch_skinny(const Params& p, hipStream_t s) {
 template <class CF>
 int launch_glds(const Params& p, hipStream_t s) {
   static std::atomic<unsigned long long> attr_set{0}, attr_simple{0};   // per device: the dynamic-LDS cap, once
-  if (p.simple) {
-    if (int e = ensure_dyn_lds((const void*)conv_glds_kernel<CF, true>, CF::LDS_BYTES, attr_simple, "conv2d")) return e;
-    hipLaunchKernelGGL((conv_glds_kernel<CF, true>), dim3(p.tiles_m * p.tiles_n, p.split), dim3(CF::NT), CF::LDS_BYTES,
+  if (p.simple == 1) {
+    if (int e = ensure_dyn_lds((const void*)conv_glds_kernel<CF, 1>, CF::LDS_BYTES, attr_simple, "conv2d")) return e;
+    hipLaunchKernelGGL((conv_glds_kernel<CF, 1>), dim3(p.tiles_m * p.tiles_n, p.split), dim3(CF::NT), CF::LDS_BYTES,
+                       s, p);
+    return check_launch("conv_glds");
+  }
+  if (p.simple == 2) {
+    static std::atomic<unsigned long long> attr_simple2{0};
+    if (int e = ensure_dyn_lds((const void*)conv_glds_kernel<CF, 2>, CF::LDS_BYTES, attr_simple2, "conv2d")) return e;
+    hipLaunchKernelGGL((conv_glds_kernel<CF, 2>), dim3(p.tiles_m * p.tiles_n, p.split), dim3(CF::NT), CF::LDS_BYTES,
                        s, p);
     return check_launch("conv_glds");
   }
@@ -2845,7 +2871,13 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
     p.nomask = g.pad == 0 && g.pad_end == 0 && !g.upsample && g.cin % BK == 0 &&
                (g.c_split == g.cin || g.c_split % BK == 0) && g.gn_scale == nullptr && !g.silu;
     // the linear K loop of the LDS-DMA kernels (conv_glds_kernel SIMPLE): one segment, one source, no masks
-    p.simple = p.nomask && a->nseg == 1 && (!g.src1 || g.c_split >= g.cin);
+    const sdk_conv_src& g1 = a->seg[1];
+    const bool one_src = !g.src1 || g.c_split >= g.cin;
+    // a second segment qualifies when it is a plain 1x1 over the output grid (the fused ResBlock shortcut)
+    const bool lin1 = a->nseg == 2 && g1.ksize == 1 && g1.stride == 1 && g1.pad == 0 && g1.pad_end == 0 &&
+                      !g1.upsample && g1.cin % BK == 0 && (!g1.src1 || g1.c_split >= g1.cin || g1.c_split % BK == 0) &&
+                      g1.gn_scale == nullptr && !g1.silu && g1.h == a->ho && g1.w == a->wo;
+    p.simple = !(p.nomask && one_src) ? 0 : a->nseg == 1 ? 1 : lin1 ? 2 : 0;
   }
   if (a->out_mode == SDK_OUT_NHWC_F16 || a->out_mode == SDK_OUT_GEGLU_F16) {
     if (a->cout % 8 || a->out_ld % 8 || (a->residual && a->res_ld % 8))

@@ -220,7 +220,10 @@ class PerImageWeights:
 def _conv_source_hash():
     import hashlib
     import os
-    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc", "conv.hip"), "rb") as f:
+    # SD_AMD_CONV_SOURCE: the conv.hip an A/B library (SD_AMD_LIB) was built from (tools only)
+    src = os.environ.get("SD_AMD_CONV_SOURCE") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc",
+                                                                "conv.hip")
+    with open(src, "rb") as f:
         return hashlib.sha1(f.read()).hexdigest()[:16]
 
 

@@ -212,3 +212,32 @@ def test_groupnorm_finalize_from_producer_statistics(ops):
     s1, t1 = ops.group_norm_scale_shift(y, gamma, beta, 1e-5, 32)
     s0, t0 = ops.group_norm_affine(y.clone(), gamma, beta, 1e-5, 32)
     assert rel_l2(s1, s0) < 1e-5 and rel_l2(t1, t0) < 1e-5
+
+
+@pytest.mark.parametrize("variant", [22, 23, 5, 7])
+@pytest.mark.parametrize("B,H,W,C0,C1,C2,Co,split", [
+    (2, 32, 32, 320, 320, 320, 320, 1),      # decoder ResBlock conv2 + 1x1 over a two-source concat
+    (1, 16, 16, 640, 1280, 0, 640, 3),       # split-K: splits start in the 3x3 and in the 1x1 segment
+    (2, 16, 16, 640, 640, 640, 1280, 2),
+])
+def test_lds_dma_fused_shortcut_segment_linear_issue(ops, variant, B, H, W, C0, C1, C2, Co, split):
+    """The LDS-DMA tile kernels on the same two-segment convs (their linear A issue, conv.hip SIMPLE = 2: three
+    per-lane row offsets, the K step's segment / source / tap offset in the scalar soffset) vs fp32, at split 1
+    and with splits that start in either segment (bitwise equality with the halo kernel at split 1:
+    test_halo_fused_shortcut_segment)."""
+    h = _rand(B, H, W, C0, seed=31)
+    a = _rand(B, H, W, C1, seed=32)
+    c = _rand(B, H, W, C2, seed=33) if C2 else None
+    g = torch.Generator().manual_seed(34)
+    w2 = torch.randn(Co, C0, 3, 3, generator=g) / math.sqrt(C0 * 9)
+    ws = torch.randn(Co, C1 + C2, 1, 1, generator=g) / math.sqrt(C1 + C2)
+    b = torch.randn(Co, generator=g) * 0.1
+    res_src = (a.to(DEV), c.to(DEV)) if C2 else a.to(DEV)
+    pc = ops.PackedConv([(w2, C0), (ws, C1 + C2)], b, device=DEV)
+    hp = _padded(h).to(DEV)
+    y, ran = _ran(ops, lambda: ops.conv2d(pc, hp, pad=0, seg2=(res_src, None, False), variant=variant, split_k=split))
+    assert ran == variant
+    xin = torch.cat([a, c], -1) if C2 else a
+    ref = (F.conv2d(h.float().permute(0, 3, 1, 2), w2.half().float(), b, padding=1) +
+           F.conv2d(xin.float().permute(0, 3, 1, 2), ws.half().float())).permute(0, 2, 3, 1)
+    assert rel_l2(y, ref) < 2e-3

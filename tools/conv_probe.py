@@ -1,5 +1,5 @@
 """Time one conv configuration (for rocprofv3 counter passes and A/B runs).
-usage: [GM=<tile_group_m>] python tools/conv_probe.py <shape> <variant> <split> [iters]
+usage: [GM=<tile_group_m>] [GN=1] python tools/conv_probe.py <shape> <variant> <split> [iters]
 shape: a tools/bench_conv.py SHAPES name, or B,H,W,Cin,Cout,k,up"""
 import os, sys
 import torch
@@ -28,7 +28,8 @@ def main():
     kw = dict(stride=st, pad=0 if name.endswith("_prepad") else k // 2, upsample=bool(up),
               variant=None if variant < 0 else variant,
               split_k=None if split <= 0 else split,
-              out_mode=ops.OUT_GEGLU_F16 if geglu else ops.OUT_NHWC_F16)
+              out_mode=ops.OUT_GEGLU_F16 if geglu else ops.OUT_NHWC_F16,
+              gn_stats=os.environ.get("GN") == "1")   # GN=1: the epilogue emits GroupNorm statistics
     y = ops.conv2d(pc, x, **kw)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
