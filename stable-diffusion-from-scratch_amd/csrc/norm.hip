@@ -11,6 +11,9 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include <map>
+#include <mutex>
+
 #include "common.h"
 
 namespace sdk {
@@ -585,6 +588,77 @@ __global__ void __launch_bounds__(256) gn_apply_pad_kernel(const half_t* s0, con
   }
 }
 
+// The same per padded row: grid (padded row, image); the image's scale / shift staged in LDS once, the row's
+// (pixel, 8-channel chunk) elements split by a host-verified multiply-shift (no 64-bit index division per
+// element), GNP_U loads in flight per thread.  Same arithmetic per element (profiles/r4_gn_apply_pad_ab.txt).
+constexpr int GNP_U = 4;
+__global__ void __launch_bounds__(256) gn_apply_pad_row_kernel(const half_t* s0, const half_t* s1, int c_split,
+                                                               int ld0, int ld1, int h, int w, int pad, int channels,
+                                                               const float* scale, const float* shift, int silu,
+                                                               half_t* y, int ldy, unsigned divm) {
+  extern __shared__ __attribute__((aligned(16))) float gst[];   // [channels] scale | [channels] shift
+  const int tid = threadIdx.x, py = blockIdx.x, b = blockIdx.y;
+  const int c8 = channels / 8, hp = h + 2 * pad, wp = w + 2 * pad;
+  for (int e = tid; e < channels / 4; e += 256) {
+    reinterpret_cast<f4*>(gst)[e] = reinterpret_cast<const f4*>(scale + (size_t)b * channels)[e];
+    reinterpret_cast<f4*>(gst + channels)[e] = reinterpret_cast<const f4*>(shift + (size_t)b * channels)[e];
+  }
+  __syncthreads();
+  const int iy = py - pad;
+  const bool row_in = (unsigned)iy < (unsigned)h;
+  const int n = wp * c8;
+  half_t* yrow = y + ((size_t)b * hp + py) * wp * (size_t)ldy;
+  const size_t pix0 = ((size_t)b * h + (row_in ? iy : 0)) * w;
+  for (int i0 = tid; i0 < n; i0 += 256 * GNP_U) {
+    h8 v[GNP_U];
+    int px[GNP_U], cc[GNP_U];
+    bool in[GNP_U];
+#pragma unroll
+    for (int u = 0; u < GNP_U; ++u) {
+      const int i = i0 + 256 * u;
+      px[u] = (int)(((unsigned long long)(unsigned)i * divm) >> 32);
+      cc[u] = (i - px[u] * c8) * 8;
+      const int ix = px[u] - pad;
+      in[u] = i < n && row_in && (unsigned)ix < (unsigned)w;
+      v[u] = in[u] ? load_px(s0, s1, c_split, ld0, ld1, pix0 + ix, cc[u]) : h8{};
+    }
+#pragma unroll
+    for (int u = 0; u < GNP_U; ++u) {
+      if (i0 + 256 * u >= n) break;
+      h8 o = {};
+      if (in[u]) {
+        const f4* ps = reinterpret_cast<const f4*>(gst + cc[u]);
+        const f4* pt = reinterpret_cast<const f4*>(gst + channels + cc[u]);
+        const f4 sa = ps[0], sb = ps[1], ta = pt[0], tb = pt[1];
+        const float sc[8] = {sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3]};
+        const float sh[8] = {ta[0], ta[1], ta[2], ta[3], tb[0], tb[1], tb[2], tb[3]};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float x = (float)v[u][j] * sc[j] + sh[j];
+          if (silu) x = x * __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+          o[j] = (half_t)x;
+        }
+      }
+      *reinterpret_cast<h8*>(yrow + (size_t)px[u] * ldy + cc[u]) = o;
+    }
+  }
+}
+
+// ceil(2^32 / d) when i * that >> 32 == i / d for every i < n (checked once per (n, d)), else 0
+unsigned pad_row_divm(int n, int d) {
+  static std::mutex mu;
+  static std::map<std::pair<int, int>, unsigned> memo;
+  std::lock_guard<std::mutex> lk(mu);
+  const auto key = std::make_pair(n, d);
+  const auto it = memo.find(key);
+  if (it != memo.end()) return it->second;
+  unsigned m = (unsigned)(((1ull << 32) + (unsigned long long)d - 1) / (unsigned long long)d);
+  for (int i = 0; i < n && m; ++i)
+    if ((int)(((unsigned long long)(unsigned)i * m) >> 32) != i / d) m = 0;
+  memo[key] = m;
+  return m;
+}
+
 // Post-activation GroupNorm of the DDPM (C1) UNet's ConvBlock / attention block:
 // y = [silu](x*scale + shift) + post_bias[b][c] + residual[pix][c] (either optional).
 __global__ void __launch_bounds__(256) gn_apply_ex_kernel(const half_t* s0, const half_t* s1, int c_split, int ld0,
@@ -785,6 +859,16 @@ extern "C" int sdk_group_norm_apply_padded(const sdk_group_norm_args* a, int32_t
     return fail(SDK_EINVAL, "group_norm_apply_padded: h*w must equal hw, pad in [0, 4]");
   const int64_t nvec = (int64_t)a->batch * (h + 2 * pad) * (w + 2 * pad) * (a->channels / 8);
   if (nvec <= 0) return SDK_OK;
+  const int hp = h + 2 * pad, wp = w + 2 * pad;
+  const unsigned divm = (int64_t)wp * (a->channels / 8) < (1 << 24) ? pad_row_divm(wp * (a->channels / 8), a->channels / 8) : 0;
+  // the row form where it measured faster (the VAE decoder's >= 128x128 images: 206.6 -> 182.5 us at 128x128x512,
+  // 696.6 -> 677.8 at 512x512x128); the grid-stride form elsewhere (64x64x640 56.6 vs 58.9 us, 16x16 17.4 vs 19.4)
+  if (divm && (int64_t)h * w >= 128 * 128 && a->channels <= 4096 && hp <= 65535 && a->batch <= 65535) {
+    hipLaunchKernelGGL(gn_apply_pad_row_kernel, dim3(hp, a->batch), dim3(256), (size_t)a->channels * 8,
+                       (hipStream_t)stream, (const half_t*)a->src0, (const half_t*)a->src1, a->c_split, a->ld0, a->ld1,
+                       h, w, pad, a->channels, a->scale, a->shift, silu, (half_t*)y, ld_y, divm);
+    return check_launch("gn_apply_pad");
+  }
   const int blocks = (int)std::min<int64_t>((nvec + 255) / 256, 8192);
   hipLaunchKernelGGL(gn_apply_pad_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const half_t*)a->src0,
                      (const half_t*)a->src1, a->c_split, a->ld0, a->ld1, h, w, pad, a->channels, a->scale, a->shift,

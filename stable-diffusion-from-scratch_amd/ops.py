@@ -235,7 +235,7 @@ class _Autotune:
     after a warm-up; SD_AMD_TUNE_REPS) and caches the fastest.  Never runs under graph capture."""
     VARIANTS = (2, 5, 7, 6, 4, 3, 8, 9, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 31, 32, 33, 34, 35, 36, 37)
     # split -2: two K halves combined inside the launch (sdk_conv_args.split_inlaunch; LDS-DMA tile kernels)
-    SPLITS = (0, 1, 2, 4, 8, -2)
+    SPLITS = (0, 1, 2, 4, 8, 12, 16, -2)
     # unsplit plans: M-panels per tile group (sdk_conv_args.tile_group_m; 1 = M-panel major)
     GROUPS = (1, 8, 16)
 
