@@ -399,6 +399,12 @@ int sdk_upsample_bilinear2x(const void* x, void* y, int32_t batch, int32_t h, in
                             sdk_stream_t stream);
 int sdk_gelu(const void* x, void* y, int64_t n, sdk_stream_t stream);
 
+/* UNet Upsample (openai_model/model.py:120-131: F.interpolate(x, scale_factor=2, mode="nearest") then
+ * conv3x3 with padding `pad`): y = [batch][2h + 2pad][2w + 2pad][channels] fp16, the nearest-x2 image with a
+ * zero border of `pad`, for an unmasked (pad 0) sdk_conv2d.  x rows have stride ld_x (halfs). */
+int sdk_upsample_nearest2x_padded(const void* x, int32_t ld_x, void* y, int32_t batch, int32_t h, int32_t w,
+                                  int32_t channels, int32_t pad, sdk_stream_t stream);
+
 /* ---------------------------------------------------------------- introspection */
 const char* sdk_last_error(void);
 int sdk_version(void);

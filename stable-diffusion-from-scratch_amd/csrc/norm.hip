@@ -644,6 +644,37 @@ __global__ void __launch_bounds__(256) gn_apply_pad_row_kernel(const half_t* s0,
   }
 }
 
+// Nearest-x2 upsample into a zero-bordered image (UNet Upsample, reference openai_model/model.py:120-131:
+// F.interpolate(scale_factor=2, mode="nearest") then the 3x3 conv with padding 1): y[b][py][px] =
+// x[b][(py - pad) >> 1][(px - pad) >> 1] inside, 0 on the border — the conv then runs unmasked (pad 0) on the
+// linear A issue instead of folding the upsample into every DMA address.  Grid (padded row, image).
+__global__ void __launch_bounds__(256) upsample_nearest2x_pad_kernel(const half_t* x, int ldx, int h, int w, int pad,
+                                                                     int channels, half_t* y, unsigned divm) {
+  const int tid = threadIdx.x, py = blockIdx.x, b = blockIdx.y;
+  const int c8 = channels / 8, hp = 2 * h + 2 * pad, wp = 2 * w + 2 * pad;
+  const int uy = py - pad;
+  const bool row_in = (unsigned)uy < (unsigned)(2 * h);
+  const int n = wp * c8;
+  half_t* yrow = y + ((size_t)b * hp + py) * wp * (size_t)channels;
+  const size_t src0 = ((size_t)b * h + (row_in ? uy >> 1 : 0)) * w;
+  for (int i0 = tid; i0 < n; i0 += 256 * GNP_U) {
+    h8 v[GNP_U];
+    int px[GNP_U], cc[GNP_U];
+#pragma unroll
+    for (int u = 0; u < GNP_U; ++u) {
+      const int i = i0 + 256 * u;
+      px[u] = (int)(((unsigned long long)(unsigned)i * divm) >> 32);
+      cc[u] = (i - px[u] * c8) * 8;
+      const int ux = px[u] - pad;
+      const bool in = i < n && row_in && (unsigned)ux < (unsigned)(2 * w);
+      v[u] = in ? *reinterpret_cast<const h8*>(x + (src0 + (ux >> 1)) * ldx + cc[u]) : h8{};
+    }
+#pragma unroll
+    for (int u = 0; u < GNP_U; ++u)
+      if (i0 + 256 * u < n) *reinterpret_cast<h8*>(yrow + (size_t)px[u] * channels + cc[u]) = v[u];
+  }
+}
+
 // ceil(2^32 / d) when i * that >> 32 == i / d for every i < n (checked once per (n, d)), else 0
 unsigned pad_row_divm(int n, int d) {
   static std::mutex mu;
@@ -1012,4 +1043,19 @@ extern "C" int sdk_group_norm(const sdk_group_norm_args* a, int32_t silu, void* 
   }
   return pad ? sdk_group_norm_apply_padded(a, silu, y, ld_y, h, w, pad, stream)
              : sdk_group_norm_apply(a, silu, y, ld_y, stream);
+}
+
+extern "C" int sdk_upsample_nearest2x_padded(const void* x, int32_t ld_x, void* y, int32_t batch, int32_t h, int32_t w,
+                                             int32_t channels, int32_t pad, sdk_stream_t stream) {
+  if (!x || !y || batch <= 0 || h <= 0 || w <= 0 || channels <= 0 || channels % 8 || ld_x % 8 || ld_x < channels ||
+      pad < 0 || pad > 4)
+    return fail(SDK_EINVAL, "upsample_nearest2x_padded: bad args (channels / ld_x multiples of 8, pad in [0, 4])");
+  const int hp = 2 * h + 2 * pad, wp = 2 * w + 2 * pad;
+  if (hp > 65535 || batch > 65535 || (int64_t)wp * (channels / 8) >= (1 << 24))
+    return fail(SDK_EINVAL, "upsample_nearest2x_padded: image too large");
+  const unsigned divm = pad_row_divm(wp * (channels / 8), channels / 8);
+  if (!divm) return fail(SDK_EINVAL, "upsample_nearest2x_padded: no exact row split");
+  hipLaunchKernelGGL(upsample_nearest2x_pad_kernel, dim3(hp, batch), dim3(256), 0, (hipStream_t)stream,
+                     (const half_t*)x, ld_x, h, w, pad, channels, (half_t*)y, divm);
+  return check_launch("upsample_nearest2x_padded");
 }

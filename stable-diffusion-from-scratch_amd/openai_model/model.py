@@ -70,8 +70,15 @@ class Downsample(nn.Module):
         return ops.conv2d(self._pc, x, stride=2, pad=self.padding, gn_stats=True)
 
 
+# the UNet Upsample materialises the nearest-x2 image zero-bordered and runs its 3x3 conv unmasked (the linear A
+# issue of the LDS-DMA kernels) instead of folding the upsample into every DMA address; SD_AMD_UPSAMPLE_FOLD=1
+# restores the folded form
+UPSAMPLE_FOLD = __import__("os").environ.get("SD_AMD_UPSAMPLE_FOLD", "0") == "1"
+
+
 class Upsample(nn.Module):
-    """Reference ``model.py:100-131``: nearest x2 (folded into the conv's loads) + conv3x3."""
+    """Reference ``model.py:100-131``: nearest x2 + conv3x3 (the upsample materialised zero-bordered, or folded
+    into the conv's loads)."""
 
     def __init__(self, channels, use_conv, dims=2, out_channels=None, padding=1):
         super().__init__()
@@ -88,7 +95,9 @@ class Upsample(nn.Module):
         self._pc = ops.PackedConv([(self.conv.weight, self.channels)], self.conv.bias, device=dev)
 
     def _run(self, x):
-        return ops.conv2d(self._pc, x, upsample=True, pad=self.padding, gn_stats=True)
+        if UPSAMPLE_FOLD or isinstance(x, tuple) or x.shape[-1] % 8:
+            return ops.conv2d(self._pc, x, upsample=True, pad=self.padding, gn_stats=True)
+        return ops.conv2d(self._pc, ops.upsample_nearest2x_padded(x, self.padding), pad=0, gn_stats=True)
 
 
 class ResBlock(TimestepBlock):

@@ -653,6 +653,19 @@ def upsample_bilinear2x(x):
     return y
 
 
+def upsample_nearest2x_padded(x, pad=1):
+    """Nearest-x2 upsample of NHWC fp16 x into a zero-bordered [B, 2H + 2pad, 2W + 2pad, C] image (the UNet
+    Upsample's interpolate; its 3x3 conv then runs with pad 0 on the unmasked linear issue)."""
+    _need_cuda(x, "upsample_nearest2x_padded")
+    B, H, W, Cc = x.shape
+    if x.stride(-1) != 1 or x.stride(1) != W * x.stride(2) or x.stride(0) != H * x.stride(1):
+        x = x.contiguous()
+    y = torch.empty(B, 2 * H + 2 * pad, 2 * W + 2 * pad, Cc, dtype=torch.float16, device=x.device)
+    check(lib().sdk_upsample_nearest2x_padded(_ptr(x), x.stride(2), _ptr(y), B, H, W, Cc, pad, _stream()),
+          "upsample_nearest2x_padded")
+    return y
+
+
 def gelu(x):
     """Exact (erf) GELU, fp16."""
     _need_cuda(x, "gelu")

@@ -632,3 +632,23 @@ def test_conv_batch_chunks_over_the_buffer_range(ops, monkeypatch):
     yn = ops.conv2d(pc, (xa, xb), seg2=(x2, None, False), out_mode=ops.OUT_NCHW_F32)
     monkeypatch.setattr(ops, "BUF_LIMIT", 2147483647)
     assert rel_l2(yn, ops.conv2d(pc, (xa, xb), seg2=(x2, None, False), out_mode=ops.OUT_NCHW_F32)) < 1e-3
+
+
+@pytest.mark.parametrize("B,H,W,C,ldx", [(2, 16, 16, 1280, 1280), (3, 8, 12, 320, 328), (1, 5, 7, 64, 64)])
+def test_upsample_nearest2x_padded(ops, B, H, W, C, ldx):
+    """sdk_upsample_nearest2x_padded (the UNet Upsample's F.interpolate(scale_factor=2, mode="nearest"),
+    reference openai_model/model.py:120-131) vs torch, zero border of 1, strided source rows; and the 3x3 conv
+    over it with pad 0 equals the conv with the upsample folded into its loads, bit for bit (same variant)."""
+    xs = _rand(B, H, W, ldx, seed=H * W + C).to(DEV)
+    x = xs[..., :C]
+    y = ops.upsample_nearest2x_padded(x, 1)
+    ref = F.pad(F.interpolate(x.float().permute(0, 3, 1, 2), scale_factor=2, mode="nearest"), (1, 1, 1, 1))
+    assert torch.equal(y.float(), ref.permute(0, 2, 3, 1))
+    if C % 64 == 0:
+        g = torch.Generator().manual_seed(C)
+        w = torch.randn(C, C, 3, 3, generator=g) / math.sqrt(9 * C)
+        pc = ops.PackedConv([(w, C)], torch.randn(C, generator=g) * 0.1, device=DEV)
+        for v in (22, 5):
+            a = ops.conv2d(pc, x.contiguous(), upsample=True, pad=1, variant=v, split_k=1)
+            b = ops.conv2d(pc, y, pad=0, variant=v, split_k=1)
+            assert torch.equal(a, b), f"variant {v}"
