@@ -24,5 +24,6 @@ run() {  # tag cmd...
 }
 run attn python3 $R/tools/bench_attn.py sd1_self_64x64_d40
 run xattn python3 $R/tools/bench_xattn.py --only sd1_64x64
-run conv python3 $R/tools/conv_probe.py unet64_320x320_3x3 22 1 5
+run conv python3 $R/tools/conv_probe.py unet64_320x320_3x3_prepad 22 1 5
+run convff1 python3 $R/tools/conv_probe.py unet32_ff1_640x5120 20 1 5
 echo PMC_DONE
