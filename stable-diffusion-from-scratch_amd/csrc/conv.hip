@@ -19,11 +19,16 @@
 // fused with the residual add.  Low-parallelism shapes (the 16x16 / 8x8 UNet
 // levels) split K across workgroups into fp32 slabs reduced by a second kernel.
 #include <algorithm>
+#include <string>
 #include <type_traits>
 #include <cstdlib>
 
 #include "common.h"
-#include "halo_sched.h"
+
+#ifndef SDK_CONV_PART
+#define SDK_CONV_PART -1
+#endif
+#define SDK_PART(k) (SDK_CONV_PART < 0 || SDK_CONV_PART == (k))
 
 namespace sdk {
 namespace {
@@ -69,14 +74,6 @@ struct Params {
                         // the LDS-DMA A gather is a lane base + a scalar tap offset, no masks
   float2* gnp;          // GroupNorm statistics of the fp16 output: [batch][gn_nch][N] (mean, M2) over
   int gn_nch;           // hw_out / gn_nch rows each (one chunk = one M-tile, or 64 rows of the split-K reduce)
-  // halo-tile 3x3 kernel (variants 36, 37; halo_sched.h): halo row stride (px), pieces per channel
-  // block, ring slots, issue schedule
-  int h_hs, h_np, h_rp;
-  int h_phi[10];
-  // GroupNorm-fused form (h_virt = 1): seg 0 is the RAW input with pad 1 (zero border virtual), its
-  // GroupNorm scale / shift (seg[0].gscale / gshift, [batch][cin]) and SiLU applied to each staged piece
-  // in LDS; halo row of pixel h = (h * h_divm) >> 20 (exact for the plan's pixel range)
-  int h_virt, h_divm;
   // in-launch split-K (LDS-DMA tile kernels, split == 2): the K halves of a tile combine inside the launch;
   // partial = one fp32 accumulator blob per (tile, half), tcnt = per-tile arrival counters (left zero)
   int inl;
@@ -324,6 +321,7 @@ __device__ __forceinline__ void epilogue(const Params& p, f16v (&acc)[FM][FN], h
     }
 }
 
+#if SDK_PART(0)   // the register-staged kernel: host planner part only
 __global__ void __launch_bounds__(NT, 2) conv_igemm_kernel(Params p) {
   __shared__ __attribute__((aligned(16))) half_t smem[4 * TILE_H];   // A0 A1 B0 B1 = 64 KiB
   half_t* As = smem;
@@ -422,6 +420,7 @@ __global__ void __launch_bounds__(NT, 2) conv_igemm_kernel(Params p) {
   const int m_w = wm * 64, n_w = wn * 64;
   epilogue<2, 2, BM, BN, NT>(p, acc, smem, m0, n0, m_w, n_w, blockIdx.y);
 }
+#endif  // SDK_PART(0)
 
 
 
@@ -1401,6 +1400,131 @@ __global__ void __launch_bounds__(CF::NT, CF::OCC * CF::NW / 4) conv_glds_kernel
   if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= CF::NT / 2) __builtin_amdgcn_s_setprio(1);
 #endif
   ph_stamp(p, 1);
+  // K loop form: the one-barrier loop with the DMA issue interleaved into the MFMAs where a SIMD holds at
+  // least two of the kernel's waves (one stalls on a DMA issue while another computes); configs with one
+  // wave per SIMD keep the two-barrier loop whose issue overlaps the other waves' finishing MFMAs (the
+  // interleaved form measured 18-23 % slower on the 4-wave 128x128 ring, +4-20 % on the 8- and 16-wave
+  // tiles: profiles/r5_glds_loop_ab.txt).  SDK_GLDS_LOOP_OLD: the two-barrier loop everywhere (A/B builds).
+#if defined(SDK_GLDS_LOOP_OLD)
+  constexpr bool ILV = false;
+#else
+  constexpr bool ILV = CF::NW * CF::OCC >= 8;
+#endif
+  if constexpr (ILV) {
+  // One barrier per K-step.  Iteration kt: wait for this wave's pieces of K-step kt (the newer NS - 2
+  // stages stay in flight), barrier (every wave's pieces of kt landed, every wave done reading the slot of
+  // kt - 1), then the MFMAs on kt with the DMA of K-step kt + NS - 1 — into the slot kt - 1 used — issued
+  // between the first MFMA groups, so the DMA issue runs under the MFMAs instead of ahead of them
+  // (round 4: ~6k cycles per 256x320 K-step for ~2.6k of MFMA, the pieces issued behind a barrier and
+  // landed before the next one).  SIMPLE plans only; the generic gather issues its stage after the barrier.
+  struct Iss {
+    __amdgpu_buffer_rsrc_t ra;
+    int toff, woff;
+    bool live, s1, sec;
+  };
+  auto stage_prep = [&](int KT) __attribute__((always_inline)) {
+    Iss q;
+    q.live = KT < kt1;
+    q.ra = d.a0;
+    q.s1 = q.sec = false;
+    q.toff = (ky * p.seg[0].w + kx) * p.seg[0].ld0 * 2 + cb * 2;
+    if constexpr (SIMPLE == 2) {
+      q.s1 = sg != 0;
+      q.sec = q.s1 && cb >= p.seg[1].c_split;
+      if (q.s1) {
+        q.toff = (cb - (q.sec ? p.seg[1].c_split : 0)) * 2;
+        q.ra = q.sec ? d.s1 : d.s0;
+      }
+    }
+    q.woff = KT * BK * 2;
+    if (q.live) ph_kadv(p, sg, ky, kx, cb);
+    return q;
+  };
+  // piece J (a compile-time index after unrolling: the per-lane offset arrays stay in registers) of the
+  // stage described by Q into ring slot BUF
+#define SDK_PIECE(Q, J, BUF)                                                                             \
+  do {                                                                                                   \
+    const int piece_ = (J) * CF::NW + wave;                                                              \
+    if (piece_ >= CF::NINSTR) {                                                                          \
+      ph_dma(d.w, lds + CF::NS * CF::STAGE_H, PH_OOB, 0);                                                \
+    } else {                                                                                             \
+      const bool a_ = piece_ * 8 < CF::TBM;                                                              \
+      unsigned base_ = cx[J];                                                                            \
+      if constexpr (SIMPLE == 2) base_ = (a_ && (Q).s1) ? ((Q).sec ? cz[J] : cy[J]) : cx[J];             \
+      ph_dma(a_ ? (Q).ra : d.w, lds + (BUF) * CF::STAGE_H + piece_ * 8 * BK, (Q).live ? base_ : PH_OOB,  \
+             a_ ? (Q).toff : (Q).woff);                                                                  \
+    }                                                                                                    \
+  } while (0)
+  for (int kt = kt0; kt < kt1; ++kt) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((CF::NS - 2) * GPW) : "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    Iss q{};
+    if constexpr (SIMPLE != 0) {
+      q = stage_prep(kt + CF::NS - 1);
+    } else {
+      SDK_STAGE(kt + CF::NS - 1, wbuf);
+    }
+    const half_t* st = lds + buf * CF::STAGE_H;
+    if constexpr (CF::M16) {
+#pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk) {
+        h8 fa[CF::FM16];
+#pragma unroll
+        for (int i = 0; i < CF::FM16; ++i)
+          fa[i] = *reinterpret_cast<const h8*>(st + swz(arow16 + i * 16, kk * 4 + c16));
+        // one W fragment at a time: the 32x160 wave tiles of the 16-wave configs keep
+        // 80 accumulator VGPRs and must stay within 128
+#pragma unroll
+        for (int j = 0; j < CF::FN16; ++j) {
+          const h8 fb = *reinterpret_cast<const h8*>(st + swz(brow16 + j * 16, kk * 4 + c16));
+#pragma unroll
+          for (int i = 0; i < CF::FM16; ++i)
+            acc16[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb, fa[i], acc16[i][j], 0, 0, 0);
+          // pieces [g * PPG, (g + 1) * PPG) after MFMA group g: all issued within the first half of the
+          // K-step's groups, so they land while the rest of it computes
+          const int g = kk * CF::FN16 + j;
+          if constexpr (SIMPLE != 0) {
+            constexpr int PPG = (2 * GPW + CF::FN16 * (BK / 32) - 1) / (CF::FN16 * (BK / 32));
+#pragma unroll
+            for (int r = 0; r < PPG; ++r)
+              if (g * PPG + r < GPW) SDK_PIECE(q, g * PPG + r < GPW ? g * PPG + r : 0, wbuf);
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < BK / 16; ++kk) {
+        h8 fa[CF::FM], fb[CF::FN];
+#pragma unroll
+        for (int i = 0; i < CF::FM; ++i)
+          fa[i] = *reinterpret_cast<const h8*>(st + swz(arow0 + i * 32, kk * 2 + fh));
+#pragma unroll
+        for (int j = 0; j < CF::FN; ++j)
+          fb[j] = *reinterpret_cast<const h8*>(st + swz(brow0 + j * 32, kk * 2 + fh));
+#pragma unroll
+        for (int i = 0; i < CF::FM; ++i) {
+#pragma unroll
+          for (int j = 0; j < CF::FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+          const int g = kk * CF::FM + i;
+          if constexpr (SIMPLE != 0) {
+            constexpr int PPG = (2 * GPW + CF::FM * (BK / 16) - 1) / (CF::FM * (BK / 16));
+#pragma unroll
+            for (int r = 0; r < PPG; ++r)
+              if (g * PPG + r < GPW) SDK_PIECE(q, g * PPG + r < GPW ? g * PPG + r : 0, wbuf);
+          }
+        }
+      }
+    }
+    buf = buf + 1 == CF::NS ? 0 : buf + 1;
+    wbuf = wbuf + 1 == CF::NS ? 0 : wbuf + 1;
+  }
+#undef SDK_PIECE
+  // (the ring becomes epilogue scratch after the post-loop barrier below: every wave's last ring read
+  // precedes its last MFMA, which precedes that barrier)
+  } else {
   for (int kt = kt0; kt < kt1; ++kt) {
     SDK_STAGE(kt + CF::NS - 1, wbuf);
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"((CF::NS - 1) * GPW) : "memory");
@@ -1446,6 +1570,7 @@ __global__ void __launch_bounds__(CF::NT, CF::OCC * CF::NW / 4) conv_glds_kernel
     __builtin_amdgcn_sched_barrier(0);
     buf = buf + 1 == CF::NS ? 0 : buf + 1;
     wbuf = wbuf + 1 == CF::NS ? 0 : wbuf + 1;
+  }
   }
 #undef SDK_STAGE
   // the trailing zero-page DMAs land before the ring is reused as epilogue scratch
@@ -1559,7 +1684,6 @@ using Cfg256x256 = Cfg<256, 256, 2, 4>;
 using Cfg256x128 = Cfg<256, 128, 4, 2>;
 using Cfg128x128 = Cfg<128, 128, 2, 2>;
 // N = 320 / 640 / 960 levels of SD: 32x160 wave tiles (5 MFMA tiles per wave)
-using Cfg256x320 = Cfg<256, 320, 8, 2>;   // 16 waves
 using Cfg256x160 = Cfg<256, 160, 8, 1>;
 using Cfg128x320 = Cfg<128, 320, 4, 2>;
 // deeper rings for tiles whose K-step is shorter than the DMA latency (~1 us issue -> landed):
@@ -1580,342 +1704,6 @@ using Cfg128x128r3m = Cfg<128, 128, 2, 2, 3, true>;
 using Cfg128x160o2m = Cfg<128, 160, 4, 1, 2, true, 2>;
 using Cfg128x128o2m = Cfg<128, 128, 2, 2, 2, true, 2>;
 using Cfg128x160r4m = Cfg<128, 160, 4, 1, 4, true>;      // one workgroup, 3 K-steps of DMA in flight
-
-// ---------------------------------------------------------------------- halo-tile 3x3 kernel
-// Variants 36 (256x320 tile, 16 waves 8x2) and 37 (128x320, 8 waves 4x2), v_mfma_f32_16x16x32_f16.
-// For a 3x3 pad-0 conv over a zero-bordered image (the GN+SiLU output of gn_apply_pad_kernel) the A
-// operand of all nine taps of a 64-channel block comes from ONE staged span of padded input rows
-// (halo_sched.h): ~np 1-KiB DMA pieces per block instead of 9 * TBM / 8, and the activation leaves
-// L2 once per block instead of nine times (SD 64x64 level, 256-pixel tile: 50 pieces vs 288).
-// W tiles stream per K-step through a 2-stage ring as in conv_glds_kernel; halo pieces stream
-// through a ring of rp slots on the host-planned schedule (the pieces of block cb+1 land while
-// block cb computes, each in the slot of a piece that is already dead).  A wave's DMA count per
-// K-step varies (its W pieces + that K-step's halo pieces), so the counted vmcnt wait is picked at
-// run time from a wave-uniform count.  Fragment reads: halo pixel h of the block sits in slot
-// (cb * np + h / 8) % rp, row h % 8, 16-B chunks XOR-swizzled with (h >> 1) & 7 (the DMA source
-// carries the same permutation) — 16 consecutive pixels hit 16 distinct bank groups.
-template <int TBM_, int TBN_, int WM_, int WN_>
-struct HCfg {
-  static constexpr int TBM = TBM_, TBN = TBN_, WM = WM_, WN = WN_;
-  static constexpr int NW = WM * WN, NT = NW * 64;
-  static constexpr int TM = TBM / WM, TN = TBN / WN;
-  static constexpr int FM16 = TM / 16, FN16 = TN / 16;
-  static constexpr int WPIECES = TBN / 8;                 // 1-KiB W pieces per K-step
-  static constexpr int WPW = (WPIECES + NW - 1) / NW;     // per wave (the last waves may issue one fewer)
-  static constexpr int WSTAGE_H = TBN * BK;               // halfs per W stage
-  static constexpr int WRING_BYTES = 2 * WSTAGE_H * 2;
-  static constexpr int VEC_BYTES = 2 * TBN * 4;           // staged bias / embedding row
-  static constexpr int GNB_BYTES = 3 * 128 * 4;           // GroupNorm scale | shift of 3 channel blocks
-  static constexpr int MAX_RP = (160 * 1024 - WRING_BYTES - VEC_BYTES - GNB_BYTES) / 1024;
-  static constexpr int APIECES = TBM / 8;                 // 1-KiB pieces of a shortcut (1x1 segment) A tile
-  static constexpr int APW = (APIECES + NW - 1) / NW;
-  static_assert(2 * TBM * BK * 2 <= MAX_RP * 1024, "two shortcut A tiles fit in the halo ring");
-  static_assert(WRING_BYTES / NW >= EPG_BYTES + TM / 16 * TN * 8, "per-wave epilogue scratch in the W ring");
-  static_assert(TBN <= NT && TBN % 8 == 0 && TM % 16 == 0 && TN % 16 == 0, "tile shape");
-};
-using HCfg256x320 = HCfg<256, 320, 8, 2>;
-using HCfg128x320 = HCfg<128, 320, 4, 2>;
-
-// s_waitcnt vmcnt(n) for a wave-uniform run-time n (waiting for fewer outstanding DMAs than needed
-// is only slower, so counts past the table wait for 12)
-__device__ __forceinline__ void vmcnt_wait_dyn(int n) {
-  switch (n) {
-#define SDK_VW(N) \
-  case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
-    SDK_VW(0) SDK_VW(1) SDK_VW(2) SDK_VW(3) SDK_VW(4) SDK_VW(5) SDK_VW(6) SDK_VW(7) SDK_VW(8) SDK_VW(9)
-    SDK_VW(10) SDK_VW(11)
-#undef SDK_VW
-    default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-  }
-}
-
-// VIRT: the GroupNorm-fused form — halo pieces are DMA'd from the raw (unpadded) input, out-of-image
-// pixels read zeros, and the K-step after a piece lands its wave applies x * scale + shift (+ SiLU) to it
-// in LDS and re-zeroes the border (the same arithmetic as gn_apply_pad_kernel, so the conv equals the
-// one over the materialised zero-bordered GN output bit for bit).  The scale / shift of a channel block
-// arrive by LDS-DMA with its first piece (3-block ring).  Single-image tiles only (one scale row).
-template <class CF, bool VIRT>
-__global__ void __launch_bounds__(CF::NT, CF::NW / 4) conv_halo_kernel(Params p) {
-  extern __shared__ __attribute__((aligned(16))) half_t lds[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / CF::WN, wn = wave % CF::WN;
-  const int nitems = p.tiles_m * p.tiles_n * p.split;
-  const int it = xcd_remap((int)blockIdx.x + (int)blockIdx.y * (int)gridDim.x, nitems);
-  int tm, tn, sidx;
-  item_coords(p, it, tm, tn, sidx);
-  const int m0 = tm * CF::TBM, n0 = tn * CF::TBN;
-  const int kt0 = sidx * p.kt_per_split, kt1 = min(p.kt_total, kt0 + p.kt_per_split);   // kt0 % 9 == 0
-  // K-steps [0, kts1): the 3x3 segment (9 per channel block); [kts1, kt_total): the fused 1x1 shortcut
-  // over the output grid (ResBlock nin_shortcut), its A tiles staged in the idle halo ring
-  const int kts1 = p.nseg > 1 ? p.seg[1].kt_begin : p.kt_total;
-  const int lrow = lane >> 3;
-  const Seg& g0 = p.seg[0];
-  const Seg& g1 = p.seg[1];
-  const DmaSrc d = make_dma_src(p, m0);
-  const int NP = p.h_np, RP = p.h_rp, HS = p.h_hs;
-  half_t* const halo = lds + 2 * CF::WSTAGE_H;
-  // the tile's halo: whole padded rows from the first output row it touches (whole images when a
-  // tile holds several); VIRT: rows of the virtually padded image (row 0 / col 0 = the zero border)
-  const int b0 = m0 / p.hw_out;
-  const int oy0 = (m0 - b0 * p.hw_out) / p.wo;
-  const int hstart = (b0 * g0.h + oy0) * g0.w;
-  const int HROWS = VIRT ? g0.h + 2 : g0.h;               // padded rows per image
-  float* const gnb = reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + CF::WRING_BYTES + RP * 1024 +
-                                              CF::VEC_BYTES);
-  // VIRT: raw source offset (bytes, or PH_OOB for the zero border) of halo pixel h, channel offset cc2
-  auto virt_src = [&](int h, unsigned ld2, unsigned cc2) __attribute__((always_inline)) {
-    const int hr = (int)(((unsigned)h * (unsigned)p.h_divm) >> 20);
-    const int hc = h - hr * HS;
-    const int r = oy0 + hr - 1, c = hc - 1;
-    const bool in = (unsigned)r < (unsigned)g0.h && (unsigned)c < (unsigned)g0.w;
-    return in ? (unsigned)((b0 * g0.h + r) * g0.w + c) * ld2 + cc2 : PH_OOB;
-  };
-  const int r16 = lane & 15, c16 = lane >> 4;
-  // halo pixel of each A fragment row (tap (0, 0)); rows past M read a valid pixel, never stored
-  int hb[CF::FM16];
-#pragma unroll
-  for (int i = 0; i < CF::FM16; ++i) {
-    const int m = min(m0 + wm * CF::TM + i * 16 + r16, p.M - 1);
-    const int b = m / p.hw_out, rem = m - b * p.hw_out;
-    const int oy = rem / p.wo, ox = rem - oy * p.wo;
-    hb[i] = ((b - b0) * HROWS + oy - oy0) * HS + ox;
-  }
-  // W pieces of this wave: tile rows 8 * (wave + NW * i) + lrow
-  unsigned wv[CF::WPW];
-#pragma unroll
-  for (int i = 0; i < CF::WPW; ++i) {
-    const int piece = wave + CF::NW * i;
-    const int rch = (lane & 7) ^ ((4 * piece + (lrow >> 1)) & 7);
-    wv[i] = piece < CF::WPIECES ? w_row_ctx(p, n0 + piece * 8 + lrow, rch) : PH_OOB;
-  }
-  const int wcnt = wave < CF::WPIECES ? (CF::WPIECES - wave + CF::NW - 1) / CF::NW : 0;
-  auto issue_w = [&](int kt, int stage) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < CF::WPW; ++i)
-      if (i < wcnt) ph_dma(d.w, lds + stage * CF::WSTAGE_H + (wave + CF::NW * i) * 8 * BK, wv[i], kt * BK * 2);
-  };
-  // shortcut A pieces of this wave: tile rows 8 * (wave + NW * i) + lrow (row-major, swizzled like W)
-  const int acnt = wave < CF::APIECES ? (CF::APIECES - wave + CF::NW - 1) / CF::NW : 0;
-  auto issue_a1 = [&](int kt, int stage) __attribute__((always_inline)) {
-    const int c = (kt - kts1) * BK;
-    const bool second = c >= g1.c_split;
-    const unsigned ld2 = (unsigned)(second ? g1.ld1 : g1.ld0) * 2u;
-    const unsigned cc2 = (unsigned)(c - (second ? g1.c_split : 0)) * 2u;
-#pragma unroll
-    for (int i = 0; i < CF::APW; ++i) {
-      const int piece = wave + CF::NW * i;
-      if (i < acnt) {
-        const int m = m0 + piece * 8 + lrow;
-        const unsigned rch = (unsigned)((lane & 7) ^ ((4 * piece + (lrow >> 1)) & 7));
-        ph_dma(second ? d.s1 : d.s0, halo + stage * CF::TBM * BK + piece * 8 * BK,
-               m < p.M ? (unsigned)m * ld2 + rch * 16u + cc2 : PH_OOB, 0);
-      }
-    }
-    return acnt;
-  };
-  // halo stream: global piece g = cb * NP + q, issued by wave (g - cb0 * NP) % NW into slot g % RP
-  const int cb0 = kt0 / 9;
-  const int gend = kt0 < kts1 ? ((min(kt1, kts1) + 8) / 9) * NP : 0;
-  int gw = cb0 * NP + wave, cbw = cb0, qw = wave, sw = gw % RP;   // this wave's next piece (NW <= NP)
-  // GroupNorm scale / shift: one buffer resource over the byte range from the lower to the higher array
-  const float* glo = VIRT ? (g0.gscale < g0.gshift ? g0.gscale : g0.gshift) : nullptr;
-  const unsigned goff_s = VIRT ? (unsigned)((const char*)g0.gscale - (const char*)glo) : 0u;
-  const unsigned goff_t = VIRT ? (unsigned)((const char*)g0.gshift - (const char*)glo) : 0u;
-  const __amdgpu_buffer_rsrc_t rgs = ph_rsrc(glo, VIRT ? (long long)(goff_s > goff_t ? goff_s : goff_t) +
-                                                          (long long)p.batch * g0.cin * 4 : 0);
-  auto issue_halo = [&](int hi) __attribute__((always_inline)) {
-    int n = 0;
-    while (gw < hi) {
-      const int c = cbw * BK;
-      const bool second = c >= g0.c_split;
-      const unsigned ld2 = (unsigned)(second ? g0.ld1 : g0.ld0) * 2u;
-      const int cc = c - (second ? g0.c_split : 0);
-      const int rchh = (lane & 7) ^ ((4 * qw + (lrow >> 1)) & 7);
-      unsigned voff;
-      if constexpr (VIRT) {
-        voff = virt_src(8 * qw + lrow, ld2, (unsigned)(cc + rchh * 8) * 2u);
-        if (qw == 0) {   // the block's GroupNorm scale / shift ride with its first piece
-          float* gb = gnb + (cbw % 3) * 128;
-          const unsigned go = (unsigned)(b0 * g0.cin + c + lane) * 4u;
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rgs, (__attribute__((address_space(3))) void*)gb, 4, go + goff_s, 0,
-                                                   0, 0);
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rgs, (__attribute__((address_space(3))) void*)(gb + 64), 4,
-                                                   go + goff_t, 0, 0, 0);
-          n += 2;
-        }
-      } else {
-        voff = (unsigned)(hstart + 8 * qw + lrow) * ld2 + (unsigned)(cc + rchh * 8) * 2u;
-      }
-      ph_dma(second ? d.a1 : d.a0, halo + sw * 512, voff, 0);
-      ++n;
-      gw += CF::NW;
-      qw += CF::NW;
-      if (qw >= NP) { qw -= NP; ++cbw; }
-      sw += CF::NW;
-      if (sw >= RP) sw -= RP;
-    }
-    return n;
-  };
-  const EpiVec ev = epi_vec_load(p, m0, n0, CF::TBM, CF::TBN);
-
-  f4 acc16[CF::FM16][CF::FN16];
-#pragma unroll
-  for (int i = 0; i < CF::FM16; ++i)
-#pragma unroll
-    for (int j = 0; j < CF::FN16; ++j) acc16[i][j] = f4{};
-  const int brow16 = wn * CF::TN + r16;
-  const int arow16 = wm * CF::TM + r16;
-
-  // VIRT: GroupNorm (+ SiLU) of n landed pieces starting at this wave's piece (g, cb, q, slot) — lane =
-  // (pixel l >> 3, logical 16-B chunk l & 7), read-modify-write in place; the border pixels become 0
-  auto transform = [&](int n, int tcb, int tq, int tsl) __attribute__((always_inline)) {
-    const int pp = lane >> 3, jc = lane & 7;
-    for (int i = 0; i < n; ++i) {
-      const int h = 8 * tq + pp;
-      const int hr = (int)(((unsigned)h * (unsigned)p.h_divm) >> 20);
-      const int hc = h - hr * HS;
-      const int r = oy0 + hr - 1, c = hc - 1;
-      const bool in = (unsigned)r < (unsigned)g0.h && (unsigned)c < (unsigned)g0.w;
-      half_t* a = halo + tsl * 512 + pp * 64 + ((jc ^ ((h >> 1) & 7)) << 3);
-      const float* gb = gnb + (tcb % 3) * 128 + jc * 8;
-      // two 4-channel halves (register budget: the 16-wave tile runs at the 128-VGPR cap)
-#pragma unroll
-      for (int hf = 0; hf < 2; ++hf) {
-        const h4 v = *reinterpret_cast<const h4*>(a + 4 * hf);
-        const f4 sc = *reinterpret_cast<const f4*>(gb + 4 * hf), sh = *reinterpret_cast<const f4*>(gb + 64 + 4 * hf);
-        h4 o = {};
-        if (in) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            float x = (float)v[k] * sc[k] + sh[k];
-            if (g0.silu) x = x * __builtin_amdgcn_rcpf(1.0f + __expf(-x));
-            o[k] = (half_t)x;
-          }
-        }
-        *reinterpret_cast<h4*>(a + 4 * hf) = o;
-      }
-      tq += CF::NW;
-      if (tq >= NP) { tq -= NP; ++tcb; }
-      tsl += CF::NW;
-      if (tsl >= RP) tsl -= RP;
-    }
-  };
-  // prologue: W of the first K-step, the first block's early halo pieces (or the first shortcut tile);
-  // VIRT: those pieces are transformed before the loop (every wave waits for its own, then a barrier)
-  issue_w(kt0, 0);
-  if (kt0 < kts1) {
-    const int pg = gw, pcb = cbw, pq = qw, psl = sw;
-    issue_halo(min(gend, cb0 * NP + p.h_phi[0]));
-    if constexpr (VIRT) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      transform((gw - pg) / CF::NW, pcb, pq, psl);
-    }
-  } else {
-    issue_a1(kt0, (kt0 - kts1) & 1);
-  }
-  int xn = 0, xcb = 0, xq = 0, xsl = 0;   // VIRT: this wave's pieces issued last K-step, transformed this one
-  int cb = cb0, j = 0;
-  int cbslot = (cb0 * NP) % RP;   // slot of the current block's piece 0
-#if !defined(SDK_NO_PRIO)
-  if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= CF::NT / 2) __builtin_amdgcn_s_setprio(1);
-#endif
-  for (int kt = kt0; kt < kt1; ++kt) {
-    const bool s1 = kt >= kts1;
-    // the first shortcut K-step after the 3x3 ones: its tile goes into the ring the last 3x3 K-step
-    // was reading (free since that K-step's closing barrier) and is waited for now
-    if (kt == kts1 && kt != kt0) issue_a1(kt, 0);
-    int n = 0;
-    if (kt + 1 < kt1) {
-      issue_w(kt + 1, (kt + 1 - kt0) & 1);
-      n = wcnt;
-      if (s1) n += issue_a1(kt + 1, (kt + 1 - kts1) & 1);
-    }
-    const int ig = gw, icb = cbw, iq = qw, isl = sw;
-    if (!s1) n += issue_halo(min(gend, cb * NP + p.h_phi[j + 1]));
-    vmcnt_wait_dyn(__builtin_amdgcn_readfirstlane(n));
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    const half_t* st = lds + ((kt - kt0) & 1) * CF::WSTAGE_H;
-    const half_t* ab[CF::FM16];
-    int sx[CF::FM16];
-    if (!s1) {
-      const int ky = j / 3, toff = ky * HS + (j - 3 * ky);
-#pragma unroll
-      for (int i = 0; i < CF::FM16; ++i) {
-        const int h = hb[i] + toff;
-        int slot = cbslot + (h >> 3);
-        slot -= slot >= RP ? RP : 0;
-        ab[i] = halo + slot * 512 + (h & 7) * 64;
-        sx[i] = (h >> 1) & 7;
-      }
-    } else {
-      const half_t* sa = halo + ((kt - kts1) & 1) * CF::TBM * BK;
-#pragma unroll
-      for (int i = 0; i < CF::FM16; ++i) {
-        const int r = arow16 + i * 16;
-        ab[i] = sa + r * BK;
-        sx[i] = (r >> 1) & 7;
-      }
-    }
-#pragma unroll
-    for (int kk = 0; kk < BK / 32; ++kk) {
-      h8 fa[CF::FM16];
-#pragma unroll
-      for (int i = 0; i < CF::FM16; ++i) fa[i] = *reinterpret_cast<const h8*>(ab[i] + (((kk * 4 + c16) ^ sx[i]) << 3));
-#pragma unroll
-      for (int jj = 0; jj < CF::FN16; ++jj) {
-        const h8 fb = *reinterpret_cast<const h8*>(st + swz(brow16 + jj * 16, kk * 4 + c16));
-#pragma unroll
-        for (int i = 0; i < CF::FM16; ++i)
-          acc16[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb, fa[i], acc16[i][jj], 0, 0, 0);
-      }
-    }
-    if constexpr (VIRT) {
-      // last K-step's pieces have landed (this K-step's wait); no K-step reads them before the next one.
-      // Placed after the MFMAs: the VALU work runs under the matrix pipe and the closing barrier's wait
-      __builtin_amdgcn_sched_barrier(0);
-      transform(xn, xcb, xq, xsl);
-      xn = (gw - ig) / CF::NW;      // pieces (the DMA count also holds a block's scale / shift)
-      xcb = icb;
-      xq = iq;
-      xsl = isl;
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();      // everyone done reading this K-step's W stage and A slots
-    __builtin_amdgcn_sched_barrier(0);
-    if (!s1 && ++j == 9) {
-      j = 0;
-      ++cb;
-      cbslot += NP;
-      cbslot -= cbslot >= RP ? RP : 0;
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  float* vec_s = reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + CF::WRING_BYTES + RP * 1024);
-  epi_vec_store(ev, vec_s, CF::TBN);
-  __builtin_amdgcn_s_barrier();
-  // the staged vectors hold zeros where there is no bias / embedding row; rb_s = nullptr only where the
-  // tile's rows span two images' embedding rows (the epilogue then reads them per row from global)
-  const float* bias_s = vec_s;
-  const float* rb_s = (ev.one_img || !p.row_bias) ? vec_s + CF::TBN : nullptr;
-  constexpr int WSCR = CF::WRING_BYTES / CF::NW / 16 * 8;   // per-wave epilogue scratch (halfs) in the W ring
-  half_t* wscr = lds + wave * WSCR;
-  const bool lds_epi = p.split == 1 && p.out_mode == SDK_OUT_NHWC_F16;
-  if (lds_epi && p.gnp) {
-    epilogue16_tile<CF::FM16, CF::FN16, true>(p, acc16, m0, n0, wm * CF::TM, wn * CF::TN, wscr, bias_s, rb_s);
-    __syncthreads();
-    gn_tile_store<CF::WM, CF::WN, CF::TN, CF::TM / 16, 16, CF::TBM, CF::TBN>(
-        p, m0, n0, [&](int w) { return reinterpret_cast<const float2*>(lds + w * WSCR + EPG_BYTES / 2); });
-  } else if (lds_epi) {
-    epilogue16_tile<CF::FM16, CF::FN16>(p, acc16, m0, n0, wm * CF::TM, wn * CF::TN, wscr, bias_s, rb_s);
-  } else {
-    epilogue16_tile_direct<CF::FM16, CF::FN16>(p, acc16, m0, n0, wm * CF::TM, wn * CF::TN, sidx);
-  }
-}
-
 
 // ---------------------------------------------------------------------- 16x16x32 epilogues
 // Transposed 16x16 accumulator (D^T = W A^T, v_mfma_f32_16x16x32_f16): lane l holds pixel
@@ -2387,6 +2175,7 @@ int launch_ph(const Params& p, hipStream_t s) {
   return check_launch("conv_ph");
 }
 
+#if SDK_PART(0)   // split-K reduces, direct and skinny kernels: host planner part only
 // Split-K reduction + epilogue: 8 columns per thread.
 // Slab sum of one (row, 8-column) octet: the slabs' 32-B pieces are loaded SK_U splits at a time
 // (independent loads in flight, instead of one dependent round trip per split) and added in split
@@ -2755,6 +2544,8 @@ int launch_skinny(const Params& p, hipStream_t s) {
   return check_launch("conv_skinny");
 }
 
+#endif  // SDK_PART(0)
+
 template <class CF>
 int launch_glds(const Params& p, hipStream_t s) {
   static std::atomic<unsigned long long> attr_set{0}, attr_simple{0};   // per device: the dynamic-LDS cap, once
@@ -2777,26 +2568,80 @@ int launch_glds(const Params& p, hipStream_t s) {
   return check_launch("conv_glds");
 }
 
-template <class CF>
-int launch_halo(const Params& p, hipStream_t s) {
-  static std::atomic<unsigned long long> attr_set{0};
-  const int kts1 = p.nseg > 1 ? p.seg[1].kt_begin : p.kt_total;
-  if (p.h_rp <= 0 || p.h_rp > CF::MAX_RP || p.h_np > p.h_rp || p.kt_per_split % 9 || kts1 % 9 ||
-      (p.nseg > 1 && p.h_rp * 1024 < 2 * CF::TBM * BK * 2))
-    return fail(SDK_EINVAL, "conv2d: halo plan out of range");
-  const int lds_bytes = CF::WRING_BYTES + p.h_rp * 1024 + CF::VEC_BYTES + (p.h_virt ? CF::GNB_BYTES : 0);
-  if (p.h_virt) {
-    static std::atomic<unsigned long long> attr_v{0};
-    if (int e = ensure_dyn_lds((const void*)conv_halo_kernel<CF, true>, 160 * 1024, attr_v, "conv2d")) return e;
-    hipLaunchKernelGGL((conv_halo_kernel<CF, true>), dim3(p.tiles_m * p.tiles_n, p.split), dim3(CF::NT), lds_bytes, s,
-                       p);
-  } else {
-    if (int e = ensure_dyn_lds((const void*)conv_halo_kernel<CF, false>, 160 * 1024, attr_set, "conv2d")) return e;
-    hipLaunchKernelGGL((conv_halo_kernel<CF, false>), dim3(p.tiles_m * p.tiles_n, p.split), dim3(CF::NT), lds_bytes,
-                       s, p);
+// ---------------------------------------------------------------------- compile partition
+// build.py compiles this file once per part (-DSDK_CONV_PART=k, in parallel; one monolithic object took
+// ~10 minutes): part 0 holds the host planner, the ABI entry points and the small kernels, parts 1-4 the
+// tile-kernel instantiations, reached through these hidden C-linkage launchers (the kernel templates are
+// visible everywhere, each is instantiated only in the part whose launcher names it).  Without
+// SDK_CONV_PART every part is in one object.
+#define SDK_HIDDEN __attribute__((visibility("hidden")))
+}  // namespace
+}  // namespace sdk
+extern "C" SDK_HIDDEN int sdk_conv_launch_part1(int v, const void* pp, void* st);
+extern "C" SDK_HIDDEN int sdk_conv_launch_part2(int v, const void* pp, void* st);
+extern "C" SDK_HIDDEN int sdk_conv_launch_part3(int v, const void* pp, void* st);
+extern "C" SDK_HIDDEN int sdk_conv_launch_part4(int v, const void* pp, void* st);
+#define SDK_PART_FN(k) extern "C" SDK_HIDDEN int sdk_conv_launch_part##k(int v, const void* pp, void* st) { \
+    using namespace sdk;                                                                                \
+    const Params& p = *static_cast<const Params*>(pp);                                                 \
+    const hipStream_t s = (hipStream_t)st;                                                              \
+    switch (v) {
+#define SDK_PART_END                                                                                    \
+    }                                                                                                   \
+    return fail(SDK_EINVAL, "conv2d: variant " + std::to_string(v) + " is not in this launcher part");  \
   }
-  return check_launch("conv_halo");
-}
+#if SDK_PART(1)
+SDK_PART_FN(1)
+    case 2: return launch_glds<Cfg256x256>(p, s);
+    case 3: return launch_glds<Cfg256x128>(p, s);
+    case 4: return launch_glds<Cfg128x128>(p, s);
+    case 6: return launch_glds<Cfg256x160>(p, s);
+    case 7: return launch_glds<Cfg128x320>(p, s);
+SDK_PART_END
+#endif
+#if SDK_PART(2)
+SDK_PART_FN(2)
+    case 16: return launch_glds<Cfg128x128r4>(p, s);
+    case 17: return launch_glds<Cfg256x128r3>(p, s);
+    case 18: return launch_glds<Cfg128x128r3>(p, s);
+    case 19: return launch_glds<Cfg128x256r3>(p, s);
+    case 22: return launch_glds<Cfg256x320m>(p, s);
+    case 23: return launch_glds<Cfg128x320m>(p, s);
+SDK_PART_END
+#endif
+#if SDK_PART(3)
+SDK_PART_FN(3)
+    case 24: return launch_glds<Cfg256x160m>(p, s);
+    case 25: return launch_glds<Cfg128x256r3m>(p, s);
+    case 26: return launch_glds<Cfg128x128r3m>(p, s);
+    case 31: return launch_glds<Cfg128x160o2m>(p, s);
+    case 32: return launch_glds<Cfg128x128o2m>(p, s);
+    case 33: return launch_glds<Cfg128x160r4m>(p, s);
+SDK_PART_END
+#endif
+#if SDK_PART(4)
+SDK_PART_FN(4)
+    case 8: return launch_ph<PhCfg8>(p, s);
+    case 9: return launch_ph<PhCfg10>(p, s);
+    case 20: return launch_ph<PhCfg8, 0, true>(p, s);    // phased 256x256, 16x16x32 MFMA
+    case 21: return launch_ph<PhCfg10, 0, true>(p, s);
+#ifdef SDK_CONV_DIAGNOSTICS
+    case 10: return launch_ph<PhCfg8, 1>(p, s);   // diagnostics: no DMA
+    case 11: return launch_ph<PhCfg8, 2>(p, s);   // diagnostics: no MFMA
+    case 12: return launch_ph<PhCfg8, 4>(p, s);   // diagnostics: DMA from the zero page
+    case 13: return launch_ph<PhCfg8, 64>(p, s);  // diagnostics: no epilogue stores
+    case 14: return launch_ph<PhCfg8, 16>(p, s);  // diagnostics: W from the zero page
+    case 15: return launch_ph<PhCfg8, 32>(p, s);  // diagnostics: A from the zero page
+    case 27: return launch_ph<PhCfg8, 128>(p, s);   // diagnostics: no W DMA issued
+    case 28: return launch_ph<PhCfg8, 256>(p, s);   // diagnostics: no A DMA issued
+    case 29: return launch_ph<PhCfg8, 512>(p, s);   // diagnostics: A DMAs read W rows (cheap addressing, L2)
+    case 30: return launch_ph<PhCfg8, 1024>(p, s);  // diagnostics: A DMAs read the centre tap (no masks/halo)
+#endif
+SDK_PART_END
+#endif
+#if SDK_PART(0)
+namespace sdk {
+namespace {
 
 #ifdef SDK_CONV_DIAGNOSTICS
 unsigned long long* g_conv_stamps = nullptr;   // 8 stamps x 65536 workgroups (SDK_CONV_STAMPS=1)
@@ -2893,15 +2738,9 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   p.res = (const half_t*)a->residual; p.res_ld = a->res_ld;
   p.out = a->out; p.out_ld = a->out_ld; p.out_mode = a->out_mode;
   bool transform = false;
-  bool transform_other = false;   // any reason but segment 0's own GroupNorm / SiLU prologue
   for (int s = 0; s < a->nseg; ++s) {
     const sdk_conv_src& g = a->seg[s];
     transform |= (g.gn_scale != nullptr) || g.silu;
-    if (s == 1) transform_other |= (g.gn_scale != nullptr) || g.silu;
-    if ((double)a->batch * g.h * g.w * std::max(g.ld0, g.ld1) * 2 >= 2147483647.0) transform_other = true;
-    if (g.c_split < g.cin && g.c_split % BK) transform_other = true;
-    if (s == 1 && (g.ksize != 1 || g.stride != 1 || g.pad != 0 || g.pad_end || g.upsample || g.h != a->ho || g.w != a->wo))
-      transform_other = true;
     // the LDS-DMA kernels: buffer resources (31-bit byte offsets), a K-step's 64 channels
     // from one concat source, and a second segment that is a plain 1x1 over the output grid
     if ((double)a->batch * g.h * g.w * std::max(g.ld0, g.ld1) * 2 >= 2147483647.0) transform = true;
@@ -2909,14 +2748,14 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
     if (s == 1 && (g.ksize != 1 || g.stride != 1 || g.pad != 0 || g.pad_end || g.upsample || g.h != a->ho || g.w != a->wo))
       transform = true;
   }
-  if ((double)((a->cout + 127) / 128 * 128) * a->k_total * 2 >= 2147483647.0) transform = transform_other = true;
-  if (a->act != SDK_ACT_NONE) transform = transform_other = true;   // the CLIP fc1 (once per prompt, not per step)
+  if ((double)((a->cout + 127) / 128 * 128) * a->k_total * 2 >= 2147483647.0) transform = true;
+  if (a->act != SDK_ACT_NONE) transform = true;   // the CLIP fc1 (once per prompt, not per step)
   // tile configuration: LDS-DMA kernels for transform-free operands, scored by
   // padded-work efficiency x whole-chip wave quantisation x measured per-config
   // throughput
   struct Opt { int variant, bm, bn, nw; double pref; bool geglu_ok; };
   // relative throughput of each config on shapes it tiles exactly (tools/bench_conv.py, MI355X)
-  const Opt opts[] = {{8, 256, 256, 8, 1.05, true}, {2, 256, 256, 8, 1.00, true}, {5, 256, 320, 16, 0.92, false},
+  const Opt opts[] = {{8, 256, 256, 8, 1.05, true}, {2, 256, 256, 8, 1.00, true}, {22, 256, 320, 16, 0.92, false},
                       {7, 128, 320, 8, 0.88, false}, {6, 256, 160, 8, 0.72, false},
                       {4, 128, 128, 4, 0.72, true}, {3, 256, 128, 8, 0.65, true}};
   int var = 0, tbm = BM, tbn = BN, best_split = 0;
@@ -3009,115 +2848,19 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
       return SDK_OK;
     }
   }
-  // variants 36 / 37: halo-tile 3x3 (256x320 / 128x320 tiles) for a pad-0 3x3 conv over a zero-bordered
-  // image (nomask, one segment); a plan exists when the tile's padded rows fit the LDS ring on time
-  // (halo_sched.h).  Forced but not applicable: the planner's choice, as for the other variants.
-  // returns 1 when the halo variant v (36 / 37) has a plan for this conv (p / info filled), 0 if not,
-  // or < 0 with an error code
-  auto try_halo = [&](int v) -> int {
-    const sdk_conv_src& g = a->seg[0];
-    // a second segment is the fused 1x1 shortcut over the output grid (transform excludes other shapes),
-    // read in whole 64-channel blocks
-    const sdk_conv_src& g1 = a->seg[1];
-    const bool seg1_ok = a->nseg == 1 || (g1.cin % BK == 0 && (g1.c_split == g1.cin || g1.c_split % BK == 0));
-    const int tbm = v == 36 ? HCfg256x320::TBM : HCfg128x320::TBM;
-    const int tbn = HCfg256x320::TBN;
-    const int nw = v == 36 ? HCfg256x320::NW : HCfg128x320::NW;
-    const int max_rp = v == 36 ? HCfg256x320::MAX_RP : HCfg128x320::MAX_RP;
-    const bool common = seg1_ok && g.ksize == 3 && g.stride == 1 && g.pad_end == 0 && !g.upsample &&
-                        a->out_mode != SDK_OUT_GEGLU_F16 && !p.wbs;
-    // physical: a pad-0 conv over a zero-bordered input; virtual (GroupNorm-fused): a pad-1 conv over the
-    // raw input with its GroupNorm scale / shift (+ SiLU), whole 64-channel blocks, single-image tiles
-    const bool phys_ok = common && !transform && g.pad == 0 && p.nomask;
-    const bool virt_ok = common && !transform_other && g.gn_scale != nullptr && g.pad == 1 && g.cin % BK == 0 &&
-                         (g.c_split == g.cin || g.c_split % BK == 0) && p.hw_out % tbm == 0;
-    HaloPlan hp;
-    int divm = 0;
-    bool ok = false;
-    if (phys_ok) {
-      ok = halo_plan(p.hw_out, p.ho, p.wo, g.h, g.w, tbm, max_rp, nw, &hp) == 0;
-    } else if (virt_ok) {
-      ok = halo_plan(p.hw_out, p.ho, p.wo, p.ho + 2, p.wo + 2, tbm, max_rp, nw, &hp, 2) == 0;
-      divm = ok ? ((1 << 20) + hp.hs - 1) / hp.hs : 0;
-      for (int h = 0; ok && h < hp.rh * hp.hs; ++h)      // the kernel's row of a halo pixel: exact here
-        ok = (int)(((unsigned)h * (unsigned)divm) >> 20) == h / hp.hs;
-    }
-    if (ok) {
-      p.variant = v;
-      p.h_virt = virt_ok && !phys_ok;
-      p.h_divm = divm;
-      p.tiles_m = (p.M + tbm - 1) / tbm;
-      p.tiles_n = (p.N + tbn - 1) / tbn;
-      p.Npad = p.tiles_n * tbn;
-      p.h_hs = hp.hs;
-      p.h_np = hp.np;
-      p.h_rp = hp.rp;
-      for (int j = 0; j < 10; ++j) p.h_phi[j] = hp.phi[j];
-      const int tiles = p.tiles_m * p.tiles_n;
-      int split = a->split_k;
-      if (split <= 0) {
-        split = 1;
-        while (tiles * split < 256 && kt / (split * 2) >= 18 && split < 16) split *= 2;
-      }
-      if (a->cout % 8) split = 1;
-      split = std::max(1, std::min(split, (kt + 8) / 9));
-      p.kt_per_split = 9 * (((kt + split - 1) / split + 8) / 9);   // split starts on 3x3 channel-block boundaries
-      split = (kt + p.kt_per_split - 1) / p.kt_per_split;
-      p.split = split;
-      p.gm = split == 1 ? tile_group_m(a, p) : 1;
-#ifdef SDK_CONV_DIAGNOSTICS
-  if (getenv("SDK_CONV_STAMPS")) {
-    if (!g_conv_stamps && (hipMalloc((void**)&g_conv_stamps, (size_t)kStampWgs * 8 * 8) != hipSuccess ||
-                           hipMemset(g_conv_stamps, 0, (size_t)kStampWgs * 8 * 8) != hipSuccess)) g_conv_stamps = nullptr;
-    if ((long long)p.tiles_m * p.tiles_n * p.split <= kStampWgs) p.stamps = g_conv_stamps;
-  }
-#endif
-      const int64_t ws = split > 1 ? (int64_t)split * p.M * p.Npad * 4 : 0;
-      int gn_nch = 0;
-      if (a->out_mode == SDK_OUT_NHWC_F16) {
-        if (split > 1) gn_nch = p.hw_out % 64 == 0 ? p.hw_out / 64 : 1;
-        else if (p.hw_out % tbm == 0) gn_nch = p.hw_out / tbm;
-      }
-      if (info) {
-        info->split_k = split;
-        info->grid_tiles = tiles;
-        info->workspace_bytes = ws;
-        info->variant = v;
-        info->flops = 2.0 * p.M * (double)p.N * kreal;
-        info->gn_chunks = gn_nch;
-      }
-      if (split > 1) p.partial = a->workspace;
-      if (a->gn_partial) {
-        if (gn_nch == 0)
-          return fail(SDK_EINVAL, "conv2d: this plan emits no GroupNorm statistics (sdk_conv_plan_info.gn_chunks == 0)");
-        p.gnp = reinterpret_cast<float2*>(a->gn_partial);
-        p.gn_nch = gn_nch;
-      }
-      return 1;
-    }
-    return 0;
-  };
-  if (forced == 36 || forced == 37) {
-    const int r = try_halo(forced);
-    if (r) return r > 0 ? SDK_OK : r;
-  } else if (forced < 0 && transform && !transform_other) {
-    // a GroupNorm (+ SiLU) prologue on a 3x3: the halo kernel applies it to its staged input (else the
-    // register-staged kernel below)
-    for (int v : {36, 37}) {
-      const int r = try_halo(v);
-      if (r) return r > 0 ? SDK_OK : r;
-    }
-  }
   // ids: 0 register-staged; 2..7 LDS-DMA configs; 8, 9 phased 256x256; 10..15 diagnostics;
   // 16..19 deep-ring LDS-DMA configs; 20, 21 phased 256x256 on v_mfma_f32_16x16x32_f16;
-  // 22..26 LDS-DMA configs 5, 7, 6, 19, 18 on v_mfma_f32_16x16x32_f16; 27..30 diagnostics;
+  // 22..26 LDS-DMA configs 256x320, 7, 6, 19, 18 on v_mfma_f32_16x16x32_f16 (5 retired); 27..30 diagnostics;
   // 31, 32 two-per-CU 128x160 / 128x128 (16x16x32); 33 128x160 with a 4-stage ring; 34 direct (<= 8 outputs).
   // The diagnostic ablations compute wrong outputs by design: the product library rejects them,
   // only the separate diagnostics build (-DSDK_CONV_DIAGNOSTICS, libsdk_amd_diag.so) runs them.
   if (is_diagnostic_variant(forced) && !kDiagnostics)
     return fail(SDK_EINVAL, "conv2d: variant " + std::to_string(forced) +
                                 " is a diagnostic ablation (only in libsdk_amd_diag.so)");
-  if (forced > 37 || forced == 1) return fail(SDK_EINVAL, "conv2d: unknown variant " + std::to_string(forced));
+  if (forced > 35 || forced == 1) return fail(SDK_EINVAL, "conv2d: unknown variant " + std::to_string(forced));
+  // variant 5 (256x320 on 32x32x16, 16 waves) spilled at the 128-VGPR cap of 4 waves per SIMD — scratch VMEM
+  // ops under hand-counted vmcnt waits; variant 22 is the same tile on 16x16x32 without spills
+  if (forced == 5) return fail(SDK_EINVAL, "conv2d: variant 5 is retired (use 22)");
   const int fbase = forced;
   const bool fvalid = forced >= 0 && forced != 1 && forced <= 33;
   const bool fgeglu = (fbase <= 4 || fbase >= 8) && fbase != 22 && fbase != 23 && fbase != 24 && fbase != 31 &&
@@ -3228,46 +2971,15 @@ extern "C" int sdk_conv2d(const sdk_conv_args* a, sdk_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
   dim3 grid(p.tiles_m * p.tiles_n, p.split);
   switch (p.variant) {
-    case 2: rc = launch_glds<Cfg256x256>(p, s); break;
-    case 3: rc = launch_glds<Cfg256x128>(p, s); break;
-    case 4: rc = launch_glds<Cfg128x128>(p, s); break;
-    case 5: rc = launch_glds<Cfg256x320>(p, s); break;
-    case 6: rc = launch_glds<Cfg256x160>(p, s); break;
-    case 7: rc = launch_glds<Cfg128x320>(p, s); break;
-    case 8: rc = launch_ph<PhCfg8>(p, s); break;
-    case 9: rc = launch_ph<PhCfg10>(p, s); break;
-#ifdef SDK_CONV_DIAGNOSTICS
-    case 10: rc = launch_ph<PhCfg8, 1>(p, s); break;   // diagnostics: no DMA
-    case 11: rc = launch_ph<PhCfg8, 2>(p, s); break;   // diagnostics: no MFMA
-    case 12: rc = launch_ph<PhCfg8, 4>(p, s); break;   // diagnostics: DMA from the zero page
-    case 13: rc = launch_ph<PhCfg8, 64>(p, s); break;  // diagnostics: no epilogue stores
-    case 14: rc = launch_ph<PhCfg8, 16>(p, s); break;  // diagnostics: W from the zero page
-    case 15: rc = launch_ph<PhCfg8, 32>(p, s); break;  // diagnostics: A from the zero page
-#endif
-    case 16: rc = launch_glds<Cfg128x128r4>(p, s); break;
-    case 17: rc = launch_glds<Cfg256x128r3>(p, s); break;
-    case 18: rc = launch_glds<Cfg128x128r3>(p, s); break;
-    case 19: rc = launch_glds<Cfg128x256r3>(p, s); break;
-    case 20: rc = launch_ph<PhCfg8, 0, true>(p, s); break;    // phased 256x256, 16x16x32 MFMA
-    case 21: rc = launch_ph<PhCfg10, 0, true>(p, s); break;
-    case 22: rc = launch_glds<Cfg256x320m>(p, s); break;
-    case 23: rc = launch_glds<Cfg128x320m>(p, s); break;
-    case 24: rc = launch_glds<Cfg256x160m>(p, s); break;
-    case 25: rc = launch_glds<Cfg128x256r3m>(p, s); break;
-    case 26: rc = launch_glds<Cfg128x128r3m>(p, s); break;
-    case 31: rc = launch_glds<Cfg128x160o2m>(p, s); break;
-    case 32: rc = launch_glds<Cfg128x128o2m>(p, s); break;
-    case 33: rc = launch_glds<Cfg128x160r4m>(p, s); break;
+    case 2: case 3: case 4: case 6: case 7: rc = sdk_conv_launch_part1(p.variant, &p, s); break;
+    case 16: case 17: case 18: case 19: case 22: case 23: rc = sdk_conv_launch_part2(p.variant, &p, s); break;
+    case 24: case 25: case 26: case 31: case 32: case 33: rc = sdk_conv_launch_part3(p.variant, &p, s); break;
+    case 8: case 9: case 20: case 21: case 10: case 11: case 12: case 13: case 14: case 15: case 27: case 28:
+    case 29: case 30:
+      rc = sdk_conv_launch_part4(p.variant, &p, s);
+      break;
     case 34: rc = launch_direct(p, s); break;
     case 35: rc = launch_skinny(p, s); break;
-    case 36: rc = launch_halo<HCfg256x320>(p, s); break;
-    case 37: rc = launch_halo<HCfg128x320>(p, s); break;
-#ifdef SDK_CONV_DIAGNOSTICS
-    case 27: rc = launch_ph<PhCfg8, 128>(p, s); break;   // diagnostics: no W DMA issued
-    case 28: rc = launch_ph<PhCfg8, 256>(p, s); break;   // diagnostics: no A DMA issued
-    case 29: rc = launch_ph<PhCfg8, 512>(p, s); break;   // diagnostics: A DMAs read W rows (cheap addressing, L2)
-    case 30: rc = launch_ph<PhCfg8, 1024>(p, s); break;  // diagnostics: A DMAs read the centre tap (no masks/halo)
-#endif
     default:
       hipLaunchKernelGGL(conv_igemm_kernel, grid, dim3(NT), 0, s, p);
       rc = check_launch("conv_igemm");
@@ -3293,3 +3005,4 @@ extern "C" int sdk_diag_conv_stamps(unsigned long long* host, long long n) {
   return hipMemcpy(host, g_conv_stamps, (size_t)n * 8, hipMemcpyDeviceToHost) == hipSuccess ? SDK_OK : SDK_EINVAL;
 }
 #endif
+#endif  // SDK_PART(0)

@@ -675,19 +675,14 @@ __global__ void __launch_bounds__(256) upsample_nearest2x_pad_kernel(const half_
   }
 }
 
-// ceil(2^32 / d) when i * that >> 32 == i / d for every i < n (checked once per (n, d)), else 0
+// ceil(2^32 / d) when i * that >> 32 == i / d for every i < n (a closed-form bound), else 0
 unsigned pad_row_divm(int n, int d) {
-  static std::mutex mu;
-  static std::map<std::pair<int, int>, unsigned> memo;
-  std::lock_guard<std::mutex> lk(mu);
-  const auto key = std::make_pair(n, d);
-  const auto it = memo.find(key);
-  if (it != memo.end()) return it->second;
-  unsigned m = (unsigned)(((1ull << 32) + (unsigned long long)d - 1) / (unsigned long long)d);
-  for (int i = 0; i < n && m; ++i)
-    if ((int)(((unsigned long long)(unsigned)i * m) >> 32) != i / d) m = 0;
-  memo[key] = m;
-  return m;
+  // m = ceil(2^32 / d) = (2^32 + e) / d with 0 <= e < d, so i * m / 2^32 = i / d + i * e / (d * 2^32): the
+  // floor is exact whenever i * e < 2^32 (frac(i / d) <= (d - 1) / d leaves 1 / d of room)
+  const unsigned long long m = ((1ull << 32) + (unsigned long long)d - 1) / (unsigned long long)d;
+  const unsigned long long e = m * (unsigned long long)d - (1ull << 32);
+  if (m > 0xffffffffull) return 0;
+  return (n <= 1 || (unsigned long long)(n - 1) * e < (1ull << 32)) ? (unsigned)m : 0u;
 }
 
 // Post-activation GroupNorm of the DDPM (C1) UNet's ConvBlock / attention block:

@@ -112,6 +112,11 @@ class ReassocContext:
 
     def weights(self):
         if self.w1 is None:
+            if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+                # the build would be recorded into the caller's graph (re-run on every replay, its
+                # matrices allocated from that graph's private pool and cached here for other graphs)
+                raise RuntimeError("ReassocContext: per-prompt weights are built eagerly — run one eager "
+                                   "step with this context before capturing a graph")
             self.w1, self.w2 = self._build()
             self._build = None
         return self.w1, self.w2

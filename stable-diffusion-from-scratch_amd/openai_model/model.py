@@ -152,19 +152,6 @@ class ResBlock(TimestepBlock):
         B, H, W, _ = ops.src_shape(x)
         c0 = (x[0] if isinstance(x, tuple) else x).shape[-1]
         c1 = x[1].shape[-1] if isinstance(x, tuple) else 0
-        if (ops.gn_conv_fusable(self._pc1, B, H, W, c0, c1) and
-                ops.gn_conv_fusable(self._pc2, B, H, W, self.out_channels, 0)):
-            # GroupNorm + SiLU applied by each 3x3 conv to its own staged input (halo-tile kernel): the
-            # normalised tensors are never written; the statistics come from the producers' epilogues
-            h = ops.conv2d(self._pc1, x, pad=1, gn=self.in_layers[0].scale_shift(x), silu=True,
-                           row_bias=(emb_all, emb_off), gn_stats=True)
-            gn2 = self.out_layers[0].scale_shift(h)
-            if self._skip_mode == "identity":
-                return ops.conv2d(self._pc2, h, pad=1, gn=gn2, silu=True, residual=x, gn_stats=True)
-            if self._skip_mode == "fused":
-                return ops.conv2d(self._pc2, h, pad=1, gn=gn2, silu=True, seg2=(x, None, False), gn_stats=True)
-            skip = ops.conv2d(self._pc_skip, x)
-            return ops.conv2d(self._pc2, h, pad=1, gn=gn2, silu=True, residual=skip, gn_stats=True)
         # GN+SiLU outputs are written zero-bordered: both 3x3 convs run with pad 0 (mask-free gather)
         gp, cp = ops.gn_conv_pad()
         xa = self.in_layers[0].norm(x, silu=True, pad=gp)

@@ -233,9 +233,10 @@ class _Autotune:
     Enabled by ``enable()`` (UNetModel/AutoEncoderKL.prepare(autotune=True)); the
     first call of each distinct problem times every candidate (HIP events, 3 reps
     after a warm-up; SD_AMD_TUNE_REPS) and caches the fastest.  Never runs under graph capture."""
-    VARIANTS = (2, 5, 7, 6, 4, 3, 8, 9, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 31, 32, 33, 34, 35, 36, 37)
+    VARIANTS = (2, 7, 6, 4, 3, 8, 9, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 31, 32, 33, 34, 35)
     # split -2: two K halves combined inside the launch (sdk_conv_args.split_inlaunch; LDS-DMA tile kernels)
-    SPLITS = (0, 1, 2, 4, 8, 12, 16, -2)
+    # (3 and 6: 80 256x256 tiles of a 16x16-level conv x 3 = 240 workgroups, one wave of the 256 CUs)
+    SPLITS = (0, 1, 2, 3, 4, 6, 8, 12, 16, -2)
     # unsplit plans: M-panels per tile group (sdk_conv_args.tile_group_m; 1 = M-panel major)
     GROUPS = (1, 8, 16)
 
@@ -291,10 +292,9 @@ class _Autotune:
             self.table[key] = (0, 0)
             return self.table[key]
         if a.seg[0].gn_scale or a.seg[0].silu:
-            # a transform prologue: the register-staged kernel, the skinny M <= 64 GEMM (SiLU on its A
-            # fragments), or the halo-tile 3x3 with GroupNorm (+ SiLU)
-            # applied to its staged input (variants 36 / 37, when a plan exists)
-            cands = (0, 35, 36, 37)
+            # a transform prologue: the register-staged kernel or the skinny M <= 64 GEMM (SiLU on its A
+            # fragments)
+            cands = (0, 35)
         best, best_t = (0, 0), float("inf")
         info = ConvPlanInfo()
         stream = _stream()
@@ -683,8 +683,8 @@ def group_norm_silu(x, gamma, beta, eps, groups=32):
 def group_norm_scale_shift(x, gamma, beta, eps, groups=32):
     """Per-(batch, channel) fp32 (scale, shift) [B, C] of GroupNorm(x) from the statistics its producing
     convs emitted (else a statistics pass) — for a 3x3 conv that applies GroupNorm + SiLU to its own
-    staged input (``conv2d(gn=(scale, shift), silu=True, pad=1)`` on the halo-tile kernel), so the
-    normalised tensor is never written (``sdk_group_norm_finalize``)."""
+    prologue (``conv2d(gn=(scale, shift), silu=True)`` on the register-staged kernel), so the normalised
+    tensor is never written (``sdk_group_norm_finalize``)."""
     args, (B, H, W, Ch), dev = _gn_args(x)
     args.groups, args.eps = groups, eps
     args.gamma, args.beta = gamma.data_ptr(), beta.data_ptr()
@@ -708,45 +708,6 @@ def group_norm_scale_shift(x, gamma, beta, eps, groups=32):
     if PROFILER.active:
         PROFILER.end()
     return scale, shift
-
-
-# Opt-in (SD_AMD_FUSED_GN_CONV=1; off by default): ResBlock 3x3 convs apply GroupNorm + SiLU to their own
-# staged input (no normalised tensor written) where the halo-tile kernel has a plan.  Off because the
-# same-box A/B lost: GroupNorm -25 ms but convs +99 ms per sample (profiles/r3_gn_fused_conv_ab.txt)
-FUSED_GN_CONV = __import__("os").environ.get("SD_AMD_FUSED_GN_CONV", "0") == "1"
-_FUSABLE = {}
-
-
-def gn_conv_fusable(pc: "PackedConv", B, H, W, c0, c1=0) -> bool:
-    """Does the halo-tile kernel take ``conv2d(pc, x, gn=..., silu=True, pad=1)`` (3x3, GroupNorm-fused) for
-    an NHWC input [B, H, W, c0] (+ a concatenated [.., c1])?  A host-side plan query (no launch), cached."""
-    if not FUSED_GN_CONV or pc.seg_geom[0][0] != 3:
-        return False
-    key = (B, H, W, c0, c1, pc.N, pc.k_total, len(pc.seg_geom))
-    hit = _FUSABLE.get(key)
-    if hit is not None:
-        return hit
-    Cin = c0 + c1
-    ok = False
-    for v in (36, 37):
-        a = ConvArgs()
-        s = a.seg[0]
-        s.src0 = 0x1000
-        s.src1 = 0x2000 if c1 else None
-        s.c_split, s.cin, s.ld0, s.ld1 = c0, Cin, c0, c1
-        s.h, s.w, s.ksize, s.stride, s.pad = H, W, 3, 1, 1
-        s.gn_scale, s.gn_shift, s.silu = 0x3000, 0x4000, 1
-        a.nseg = 1
-        a.batch, a.ho, a.wo, a.cout = B, H, W, pc.N
-        a.weight, a.out, a.out_ld, a.out_mode = 0x5000, 0x6000, pc.N, OUT_NHWC_F16
-        a.k_total = pc.seg_geom[0][1] // BK * BK * 9 if pc.seg_geom[0][1] % BK == 0 else -1
-        a.variant_hint = v + 1
-        info = ConvPlanInfo()
-        if a.k_total > 0 and lib().sdk_conv2d_plan(C.byref(a), C.byref(info)) == 0 and info.variant == v:
-            ok = True
-            break
-    _FUSABLE[key] = ok
-    return ok
 
 
 def group_norm_affine(x, gamma, beta, eps, groups=32):

@@ -42,7 +42,7 @@ def _conv_ref(x_nhwc, w, b, stride=1, pad=1, upsample=False, gn=None, silu=False
     return F.conv2d(x, w.float(), None if b is None else b.float(), stride=stride, padding=pad).permute(0, 2, 3, 1)
 
 
-@pytest.fixture(params=["auto", "0", "2", "3", "4", "5", "6", "7", "8", "9", "16", "17", "18", "19", "20", "21",
+@pytest.fixture(params=["auto", "0", "2", "3", "4", "6", "7", "8", "9", "16", "17", "18", "19", "20", "21",
                         "22", "23", "24", "25", "26", "31", "32", "33"])
 def conv_variant(request, sdk):
     """Every conv kernel variant (register-staged 128x128, LDS-DMA 256x256/256x128/128x128)."""
@@ -333,7 +333,7 @@ def test_group_norm_apply_concat(ops, silu):
     assert rel_l2(y, ref.permute(0, 2, 3, 1)) < 1e-3
 
 
-GLDS_VARIANTS = {2, 3, 4, 5, 6, 7, 16, 17, 18, 19, 22, 23, 24, 25, 26, 31, 32, 33}
+GLDS_VARIANTS = {2, 3, 4, 6, 7, 16, 17, 18, 19, 22, 23, 24, 25, 26, 31, 32, 33}
 
 
 def _chunk_stats(y, nch):
@@ -362,7 +362,8 @@ def test_conv_emits_group_norm_statistics(ops, conv_variant, H, W, Ci, Co, split
     assert rel_l2(y, ref) < 3e-3
     part = getattr(y, ops.GN_ATTR, None)
     forced = None if conv_variant == "auto" else int(conv_variant)
-    if split or forced is None or forced in GLDS_VARIANTS:
+    # the phased 32x32x16 kernel (8 / 9) emits from its epilogue when its 256-row tiles stay inside one image
+    if split or forced is None or forced in GLDS_VARIANTS or (forced in (8, 9) and (H * W) % 256 == 0):
         assert part is not None, "this plan should emit GroupNorm statistics"
     if part is None:
         return

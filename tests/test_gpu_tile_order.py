@@ -51,7 +51,7 @@ def test_geglu_gemm_order_invariant(ops, variant):
     assert rel_l2(outs[1][:2048], ref) < 3e-3
 
 
-@pytest.mark.parametrize("variant", (36, 5))
+@pytest.mark.parametrize("variant", (22, 24))
 def test_conv3x3_order_invariant_with_gn_stats(ops, variant):
     B, H, W, Ci, Co = 16, 64, 64, 320, 320
     x = _rand(B, H + 2, W + 2, Ci, seed=4).to(DEV)

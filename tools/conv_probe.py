@@ -27,7 +27,7 @@ def main():
     pc = ops.PackedConv([(w, Ci)], torch.zeros(Co, device="cuda"), geglu=bool(geglu), device="cuda")
     kw = dict(stride=st, pad=0 if name.endswith("_prepad") else k // 2, upsample=bool(up),
               variant=None if variant < 0 else variant,
-              split_k=None if split <= 0 else split,
+              split_k=None if split == 0 else split,   # -2: in-launch split-K
               out_mode=ops.OUT_GEGLU_F16 if geglu else ops.OUT_NHWC_F16,
               gn_stats=os.environ.get("GN") == "1")   # GN=1: the epilogue emits GroupNorm statistics
     y = ops.conv2d(pc, x, **kw)
