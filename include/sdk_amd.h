@@ -204,6 +204,9 @@ int sdk_group_norm_apply_ex(const sdk_group_norm_args* a, int32_t silu, const fl
 double sdk_probe_mfma_flops(int32_t m16, int32_t blocks, int32_t iters);
 int sdk_probe_mfma(int32_t m16, int32_t blocks, int32_t iters, const void* seed, float* sink, sdk_stream_t stream);
 int sdk_probe_copy(const void* src, void* dst, int64_t bytes, sdk_stream_t stream);
+/* the copy with its shape chosen: mode bit 0 = 8 loads in flight per thread (else 4), bit 1 = non-temporal
+   loads / stores, bits 2-7 = workgroups per CU (0: 16); sdk_probe_copy is mode 0 */
+int sdk_probe_copy_ex(const void* src, void* dst, int64_t bytes, int32_t mode, sdk_stream_t stream);
 
 /* ---------------------------------------------------------------- LayerNorm
  * y = (x - mean) * rstd * gamma + beta over the last dim, fp16 in/out, fp32 math; gamma / beta fp32,

@@ -85,7 +85,7 @@ EXPORTS = ["sdk_conv2d_plan", "sdk_conv2d", "sdk_group_norm_workspace", "sdk_gro
            "sdk_attention", "sdk_cross_attention_block_supported", "sdk_cross_attention_block", "sdk_cross_attention_block_ln", "sdk_segment_softmax", "sdk_ff_supported", "sdk_ff_packed_bytes", "sdk_ff_pack", "sdk_feed_forward", "sdk_token_linear_supported", "sdk_token_linear", "sdk_token_linear_ln", "sdk_ddim_step", "sdk_ddpm_step", "sdk_timestep_embedding", "sdk_nchw_to_nhwc",
            "sdk_diag_gaussian_sample", "sdk_stochastic_encode", "sdk_token_embedding", "sdk_extract_patches",
            "sdk_fold_patches", "sdk_upsample_bilinear2x", "sdk_upsample_nearest2x_padded", "sdk_gelu", "sdk_last_error", "sdk_version", "sdk_kernel_name",
-           "sdk_probe_mfma_flops", "sdk_probe_mfma", "sdk_probe_copy"]
+           "sdk_probe_mfma_flops", "sdk_probe_mfma", "sdk_probe_copy", "sdk_probe_copy_ex"]
 
 _lib = None
 
@@ -141,6 +141,7 @@ def lib():
     L.sdk_probe_mfma_flops.restype = C.c_double
     L.sdk_probe_mfma.argtypes = [i32, i32, i32, vp, vp, vp]
     L.sdk_probe_copy.argtypes = [vp, vp, i64, vp]
+    L.sdk_probe_copy_ex.argtypes = [vp, vp, i64, i32, vp]
     L.sdk_last_error.restype = C.c_char_p
     L.sdk_kernel_name.restype = C.c_char_p
     L.sdk_kernel_name.argtypes = [i32]

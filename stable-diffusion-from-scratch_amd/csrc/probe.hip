@@ -52,16 +52,21 @@ __global__ void __launch_bounds__(256) mfma_probe_kernel(const half_t* seed, int
   if (lane == 0) sink[blockIdx.x * 4 + (threadIdx.x >> 6)] = r;
 }
 
-// 4 independent 16-B loads in flight per thread, then their stores
+// U independent 16-B loads in flight per thread, then their stores; NT: non-temporal loads and stores
+// (streamed once: no cache allocation on the way through)
+template <int U, bool NT>
 __global__ void __launch_bounds__(256) copy_probe_kernel(const h8* src, h8* dst, int64_t n) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  for (; i + 3 * stride < n; i += 4 * stride) {
-    h8 v[4];
+  for (; i + (U - 1) * stride < n; i += U * stride) {
+    h8 v[U];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = src[i + u * stride];
+    for (int u = 0; u < U; ++u) v[u] = NT ? __builtin_nontemporal_load(src + i + u * stride) : src[i + u * stride];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) dst[i + u * stride] = v[u];
+    for (int u = 0; u < U; ++u) {
+      if constexpr (NT) __builtin_nontemporal_store(v[u], dst + i + u * stride);
+      else dst[i + u * stride] = v[u];
+    }
   }
   for (; i < n; i += stride) dst[i] = src[i];
 }
@@ -156,10 +161,24 @@ extern "C" int sdk_probe_mfma(int32_t m16, int32_t blocks, int32_t iters, const 
   return check_launch("probe_mfma");
 }
 
-extern "C" int sdk_probe_copy(const void* src, void* dst, int64_t bytes, sdk_stream_t stream) {
-  if (!src || !dst || bytes <= 0 || bytes % 16) return fail(SDK_EINVAL, "probe_copy: bad arguments");
+// mode: bit 0 = 8 loads in flight per thread (else 4), bit 1 = non-temporal, bits 2-7 = workgroups per CU (0: 16)
+extern "C" int sdk_probe_copy_ex(const void* src, void* dst, int64_t bytes, int32_t mode, sdk_stream_t stream) {
+  if (!src || !dst || bytes <= 0 || bytes % 16 || mode < 0) return fail(SDK_EINVAL, "probe_copy: bad arguments");
   const int64_t n = bytes / 16;
-  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 256 * 16);
-  hipLaunchKernelGGL(copy_probe_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const h8*)src, (h8*)dst, n);
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int per_cu = (mode >> 2) & 63 ? (mode >> 2) & 63 : 16;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, (int64_t)cus * per_cu);
+  const hipStream_t s = (hipStream_t)stream;
+  switch (mode & 3) {
+    case 0: hipLaunchKernelGGL((copy_probe_kernel<4, false>), dim3(blocks), dim3(256), 0, s, (const h8*)src, (h8*)dst, n); break;
+    case 1: hipLaunchKernelGGL((copy_probe_kernel<8, false>), dim3(blocks), dim3(256), 0, s, (const h8*)src, (h8*)dst, n); break;
+    case 2: hipLaunchKernelGGL((copy_probe_kernel<4, true>), dim3(blocks), dim3(256), 0, s, (const h8*)src, (h8*)dst, n); break;
+    default: hipLaunchKernelGGL((copy_probe_kernel<8, true>), dim3(blocks), dim3(256), 0, s, (const h8*)src, (h8*)dst, n); break;
+  }
   return check_launch("probe_copy");
+}
+
+extern "C" int sdk_probe_copy(const void* src, void* dst, int64_t bytes, sdk_stream_t stream) {
+  return sdk_probe_copy_ex(src, dst, bytes, 0, stream);
 }

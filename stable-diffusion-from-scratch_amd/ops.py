@@ -794,33 +794,45 @@ def probe_peaks(reps=3):
     dev = torch.device("cuda", torch.cuda.current_device())
     seed = torch.randn(32768, device=dev).half()
     nsm = torch.cuda.get_device_properties(dev).multi_processor_count
-    blocks = 2 * nsm
-    sink = torch.empty(blocks * 4, dtype=torch.float32, device=dev)
+    sink = torch.empty(4 * nsm * 4, dtype=torch.float32, device=dev)
     out = {}
+    # 2 or 4 workgroups of 4 waves per CU (2 / 4 waves per SIMD): the faster is the ceiling
     for m16, iters, name in ((1, 40000, "mfma_16x16x32_f16_tflops"), (0, 20000, "mfma_32x32x16_f16_tflops")):
-        check(lib().sdk_probe_mfma(m16, blocks, 200, _ptr(seed), _ptr(sink), _stream()), "probe_mfma")
+        top = 0.0
+        for blocks in (2 * nsm, 4 * nsm):
+            check(lib().sdk_probe_mfma(m16, blocks, 200, _ptr(seed), _ptr(sink), _stream()), "probe_mfma")
+            best = float("inf")
+            for _ in range(reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                check(lib().sdk_probe_mfma(m16, blocks, iters, _ptr(seed), _ptr(sink), _stream()), "probe_mfma")
+                e1.record()
+                e1.synchronize()
+                best = min(best, e0.elapsed_time(e1))
+            top = max(top, lib().sdk_probe_mfma_flops(m16, blocks, iters) / (best * 1e-3) / 1e12)
+        out[name] = round(top, 1)
+    # HBM: a 1 GiB copy (read + write counted), the best of a few shapes — loads in flight per thread,
+    # non-temporal or default policy, workgroups per CU (the fastest is the device's streaming ceiling)
+    nbytes = 1 << 30
+    src = torch.empty(nbytes // 2, dtype=torch.float16, device=dev).normal_()
+    dst = torch.empty_like(src)
+    best_gbs, best_mode = 0.0, 0
+    for mode in (0, 1, 2, 3, 1 | (8 << 2), 3 | (8 << 2), 1 | (32 << 2), 3 | (32 << 2)):
+        check(lib().sdk_probe_copy_ex(_ptr(src), _ptr(dst), nbytes, mode, _stream()), "probe_copy")
         best = float("inf")
         for _ in range(reps):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            check(lib().sdk_probe_mfma(m16, blocks, iters, _ptr(seed), _ptr(sink), _stream()), "probe_mfma")
+            check(lib().sdk_probe_copy_ex(_ptr(src), _ptr(dst), nbytes, mode, _stream()), "probe_copy")
             e1.record()
             e1.synchronize()
             best = min(best, e0.elapsed_time(e1))
-        out[name] = round(lib().sdk_probe_mfma_flops(m16, blocks, iters) / (best * 1e-3) / 1e12, 1)
-    nbytes = 1 << 30
-    src = torch.empty(nbytes // 2, dtype=torch.float16, device=dev).normal_()
-    dst = torch.empty_like(src)
-    check(lib().sdk_probe_copy(_ptr(src), _ptr(dst), nbytes, _stream()), "probe_copy")
-    best = float("inf")
-    for _ in range(reps):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        check(lib().sdk_probe_copy(_ptr(src), _ptr(dst), nbytes, _stream()), "probe_copy")
-        e1.record()
-        e1.synchronize()
-        best = min(best, e0.elapsed_time(e1))
-    out["hbm_copy_gbs"] = round(2 * nbytes / (best * 1e-3) / 1e9, 1)
+        gbs = 2 * nbytes / (best * 1e-3) / 1e9
+        if gbs > best_gbs:
+            best_gbs, best_mode = gbs, mode
+    out["hbm_copy_gbs"] = round(best_gbs, 1)
+    out["hbm_copy_mode"] = {"loads_in_flight": 8 if best_mode & 1 else 4, "nontemporal": bool(best_mode & 2),
+                            "workgroups_per_cu": (best_mode >> 2) or 16}
     del src, dst
     return out
 

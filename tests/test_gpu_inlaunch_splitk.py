@@ -14,7 +14,7 @@ from gpu_util import rel_l2
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-TILE_VARIANTS = (2, 3, 4, 5, 6, 7, 16, 17, 18, 19, 22, 23, 24, 25, 26, 31, 32, 33)
+TILE_VARIANTS = (2, 3, 4, 6, 7, 16, 17, 18, 19, 22, 23, 24, 25, 26, 31, 32, 33)
 
 
 @pytest.fixture(scope="module")
@@ -54,7 +54,7 @@ def test_inlaunch_token_gemm_equals_slab_split(ops, variant):
     assert int(ops.WORKSPACE.counters(DEV).abs().sum().item()) == 0
 
 
-@pytest.mark.parametrize("variant", (5, 7, 22, 23, 19, 25))
+@pytest.mark.parametrize("variant", (2, 7, 22, 23, 19, 25))
 def test_inlaunch_conv3x3_group_norm_statistics(ops, variant):
     """A 16x16 ResBlock 3x3 conv (640 -> 1280, bias + embedding row + residual) combined in-launch emits its
     GroupNorm statistics per M-tile like an unsplit tile; group_norm from them equals a statistics pass."""

@@ -649,7 +649,7 @@ def test_upsample_nearest2x_padded(ops, B, H, W, C, ldx):
         g = torch.Generator().manual_seed(C)
         w = torch.randn(C, C, 3, 3, generator=g) / math.sqrt(9 * C)
         pc = ops.PackedConv([(w, C)], torch.randn(C, generator=g) * 0.1, device=DEV)
-        for v in (22, 5):
+        for v in (22, 2):
             a = ops.conv2d(pc, x.contiguous(), upsample=True, pad=1, variant=v, split_k=1)
             b = ops.conv2d(pc, y, pad=0, variant=v, split_k=1)
             assert torch.equal(a, b), f"variant {v}"
