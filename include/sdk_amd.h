@@ -112,7 +112,7 @@ typedef struct {
                               GroupNorm statistics included): no reduce kernel, no slab round trip through it */
   uint32_t* tile_counters; /* with split_inlaunch: >= SDK_TILE_COUNTERS zero-initialised words, one arrival
                               counter per output tile (device memory); every launch leaves them zero */
-  int32_t tile_group_m;    /* unsplit LDS-DMA / phased / halo plans: output tiles are visited in groups of this
+  int32_t tile_group_m;    /* unsplit LDS-DMA / phased plans: output tiles are visited in groups of this
                               many M-panels, N-tile major inside a group, so the tiles co-resident on one XCD
                               share both their A panels and their W tiles in its L2; 0: the library's choice,
                               1: M-panel major (every N-tile of a panel, then the next panel) */
@@ -183,9 +183,9 @@ int sdk_group_norm(const sdk_group_norm_args* a, int32_t silu, void* y, int32_t 
 
 /* The statistics half of sdk_group_norm alone: a->scale / a->shift [batch][channels] of the
  * GroupNorm affine, merged from the producers' per-chunk statistics (part0 / part1 as above) or, with
- * none, computed from x (sdk_group_norm_affine).  For a 3x3 conv that applies GroupNorm + SiLU to its
- * own A operand (sdk_conv_src.gn_scale / gn_shift / silu with pad 1: the halo-tile conv, variants
- * 36 / 37), so the normalised tensor is never written. */
+ * none, computed from x (sdk_group_norm_affine).  For a conv that applies GroupNorm + SiLU to its own
+ * A operand (sdk_conv_src.gn_scale / gn_shift / silu: the transform-prologue plans, variants 0 / 35),
+ * so the normalised tensor is never written. */
 int sdk_group_norm_finalize(const sdk_group_norm_args* a, const float* part0, int32_t nch0, const float* part1,
                             int32_t nch1, sdk_stream_t stream);
 

@@ -29,7 +29,7 @@ if [ "${SKIP_TUNE:-0}" != "1" ]; then
   cp $T configs/conv_tuning_mi355x.json
 fi
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
-  step tests 1500 python -u -m pytest tests -m gpu -v --timeout 400 --timeout-method thread
+  step tests 1100 python -u -m pytest tests -m gpu -v -s --timeout 400 --timeout-method thread
 fi
 step bench_c3 600 env BENCH_SHAPES_OUT=$O/shapes.txt python -u bench.py --steps 5 --warmup 2
 step bench_c5 600 python -u bench.py --config c5 --steps 2 --warmup 1

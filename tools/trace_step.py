@@ -2,6 +2,7 @@
 between consecutive kernels, and the step's wall span.
 
 usage: python tools/trace_step.py <run_kernel_trace.csv> [step_index] [--list] [--seq seq.json]
+(step_index default: len(steps) // 4, a graph-replayed step of the bench's warm-up sample)
 --seq: the launch sequence of one UNet forward written by bench.py (BENCH_SEQ_OUT); each
 record is paired in order with its dispatches (conv [+ splitk_reduce], GN partial+finalize, ...)
 and a per-shape table of device times is printed.
@@ -25,8 +26,10 @@ def short(n):
 def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    idx = int(sys.argv[2]) if len(sys.argv) > 2 and not sys.argv[2].startswith("-") else -3
     marks = [i for i, r in enumerate(rows) if "ddim_step_kernel" in r["Kernel_Name"]]
+    # default: a step inside the warm-up sample's graph replays (a quarter into the run — not the last steps,
+    # which belong to bench.py's eager, event-instrumented profiling pass)
+    idx = int(sys.argv[2]) if len(sys.argv) > 2 and not sys.argv[2].startswith("-") else max(1, len(marks) // 4)
     a, b = marks[idx - 1] + 1, marks[idx] + 1
     step = rows[a:b]
     t0, t1 = int(step[0]["Start_Timestamp"]), int(step[-1]["End_Timestamp"])
