@@ -71,6 +71,27 @@ __global__ void __launch_bounds__(256) copy_probe_kernel(const h8* src, h8* dst,
   for (; i < n; i += stride) dst[i] = src[i];
 }
 
+// The flat form: one pass, no loop — workgroup b copies its own contiguous 256*U-vector chunk (each
+// wave-instruction 1 KiB contiguous), the grid covers the buffer
+template <int U, bool NT>
+__global__ void __launch_bounds__(256) copy_flat_kernel(const h8* src, h8* dst, int64_t n) {
+  const int64_t base = (int64_t)blockIdx.x * 256 * U + threadIdx.x;
+  h8 v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = base + u * 256;
+    if (i < n) v[u] = NT ? __builtin_nontemporal_load(src + i) : src[i];
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = base + u * 256;
+    if (i < n) {
+      if constexpr (NT) __builtin_nontemporal_store(v[u], dst + i);
+      else dst[i] = v[u];
+    }
+  }
+}
+
 // LDS-DMA fill rate (diagnostic, tools/probe_dma.py): every wave of a workgroup streams 1-KiB pieces
 // (64 lanes x 16 B, one buffer_load ... lds) from `src` into its own LDS ring, keeping INF pieces in
 // flight (counted vmcnt), `pieces` per wave; consecutive waves / workgroups read consecutive pieces,
@@ -161,7 +182,8 @@ extern "C" int sdk_probe_mfma(int32_t m16, int32_t blocks, int32_t iters, const 
   return check_launch("probe_mfma");
 }
 
-// mode: bit 0 = 8 loads in flight per thread (else 4), bit 1 = non-temporal, bits 2-7 = workgroups per CU (0: 16)
+// mode: bit 0 = 8 loads in flight per thread (else 4), bit 1 = non-temporal, bits 2-7 = workgroups per CU (0: 16);
+// bit 8: the flat one-pass form (bits 2-7 ignored: the grid covers the buffer)
 extern "C" int sdk_probe_copy_ex(const void* src, void* dst, int64_t bytes, int32_t mode, sdk_stream_t stream) {
   if (!src || !dst || bytes <= 0 || bytes % 16 || mode < 0) return fail(SDK_EINVAL, "probe_copy: bad arguments");
   const int64_t n = bytes / 16;
@@ -170,6 +192,18 @@ extern "C" int sdk_probe_copy_ex(const void* src, void* dst, int64_t bytes, int3
   const int per_cu = (mode >> 2) & 63 ? (mode >> 2) & 63 : 16;
   const int blocks = (int)std::min<int64_t>((n + 255) / 256, (int64_t)cus * per_cu);
   const hipStream_t s = (hipStream_t)stream;
+  if (mode & 256) {
+    const int u = (mode & 1) ? 8 : 4;
+    const int64_t fb = (n + 256 * u - 1) / (256 * u);
+    if (fb > 0x7fffffffLL) return fail(SDK_EINVAL, "probe_copy: buffer too large for the flat form");
+    switch (mode & 3) {
+      case 0: hipLaunchKernelGGL((copy_flat_kernel<4, false>), dim3((unsigned)fb), dim3(256), 0, s, (const h8*)src, (h8*)dst, n); break;
+      case 1: hipLaunchKernelGGL((copy_flat_kernel<8, false>), dim3((unsigned)fb), dim3(256), 0, s, (const h8*)src, (h8*)dst, n); break;
+      case 2: hipLaunchKernelGGL((copy_flat_kernel<4, true>), dim3((unsigned)fb), dim3(256), 0, s, (const h8*)src, (h8*)dst, n); break;
+      default: hipLaunchKernelGGL((copy_flat_kernel<8, true>), dim3((unsigned)fb), dim3(256), 0, s, (const h8*)src, (h8*)dst, n); break;
+    }
+    return check_launch("probe_copy");
+  }
   switch (mode & 3) {
     case 0: hipLaunchKernelGGL((copy_probe_kernel<4, false>), dim3(blocks), dim3(256), 0, s, (const h8*)src, (h8*)dst, n); break;
     case 1: hipLaunchKernelGGL((copy_probe_kernel<8, false>), dim3(blocks), dim3(256), 0, s, (const h8*)src, (h8*)dst, n); break;

@@ -6,7 +6,8 @@ The bench line (C3) is produced by: B = 16, the committed conv tuning table
 query rows, i.e. B = 16 at the 64x64 level) and HIP-graph replay of the UNet, reached through
 LatentDiffusion.apply_model → DiffusionWrapper.forward.  These tests build the model with
 bench.py's own ``build_models`` and check that configuration against the fp32 CPU oracle on
-samples 0 and 15 (rel-L2 <= 5e-3 and max-abs <= 2e-2 of the range: fp16 activations, fp32 accumulation), graph replay against
+samples 0 and 15 (rel-L2 <= 5e-3 and max-abs <= 7e-3 of the range, ~3x the measured: fp16 activations, fp32
+accumulation), graph replay against
 eager launches (bitwise), and run-to-run determinism (bitwise).
 
 Cache soundness (reference ``ldm/diffusion/ddim.py:168-206``): the context K/V cache and the
@@ -85,7 +86,7 @@ def test_bench_config_unet_vs_oracle_samples_0_and_15(bench_c3):
     torch.set_num_threads(16)
     for i in (0, 15):
         ref = unet_forward(sd, bench_c3["cfg"]["unet"], xT[i:i + 1].cpu(), torch.tensor([501]), ctx[i:i + 1].cpu())
-        check_parity(f"C3 bench-config UNet sample {i}", y[i:i + 1], ref)
+        check_parity(f"C3 bench-config UNet sample {i}", y[i:i + 1], ref, 5e-3, 7e-3)   # measured 2.04e-3 / 2.13e-3
 
 
 def test_bench_config_graph_replay_equals_eager_bitwise(bench_c3):

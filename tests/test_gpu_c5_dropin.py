@@ -3,8 +3,8 @@
 
 * C5 (BASELINE configs[4]): the SD-2-shape UNet (``num_head_channels: 64``, context 1024,
   ``openai_model/model.py:289-315``) at a 96x96 latent — 9,216-token self-attention at d = 64 —
-  and the 96² → 768² VAE decode, each at B = 1 vs the fp32 CPU oracle (rel-L2 <= 5e-3, max-abs <= 2e-2 of
-  the range).
+  and the 96² → 768² VAE decode, each at B = 1 vs the fp32 CPU oracle (limits per test, ~3x the measured
+  errors of profiles/r5_parity_errors.txt).
 * v-prediction is an extension (the reference has eps / x0 only, ``Diffusion/ddpm.py:131``;
   SURVEY Q9): ε = √ᾱ·v + √(1-ᾱ)·x inside the fused DDIM update, bit-exact vs the oracle's
   restatement ``oracle.schedule.v_to_eps`` — PARITY UNPINNED (no reference value exists).
@@ -59,7 +59,7 @@ def test_c5_sd2_unet_96_latent_vs_oracle(sdk):
     torch.set_num_threads(16)
     ref = unet_forward(sd, SD2, x, t, ctx)
     assert y.shape == (1, 4, 96, 96)
-    check_parity("C5 SD-2 UNet 96x96", y, ref)
+    check_parity("C5 SD-2 UNet 96x96", y, ref, 5e-3, 6e-3)   # measured 1.60e-3 / 1.87e-3
 
 
 def test_c5_vae_decode_96_to_768_vs_oracle(sdk):
@@ -73,7 +73,7 @@ def test_c5_vae_decode_96_to_768_vs_oracle(sdk):
     torch.set_num_threads(16)
     ref = decode_first_stage(sd, SD_VAE, z, 0.18215)
     assert dec.shape == (1, 3, 768, 768)
-    check_parity("C5 VAE decode 96->768", dec, ref)
+    check_parity("C5 VAE decode 96->768", dec, ref, 3.5e-3, 4e-3)   # measured 1.09e-3 / 1.15e-3
 
 
 @pytest.mark.parametrize("index", [0, 7, 25, 49])

@@ -199,6 +199,8 @@ def test_layer_norm_rows_walk_and_offset_mean(ops, M, C, offset):
 @pytest.mark.parametrize("B,H,nq,nk,d", [
     (2, 8, 300, 300, 40), (1, 8, 256, 77, 80), (1, 8, 64, 64, 160), (2, 5, 200, 77, 64),
     (1, 2, 100, 100, 8), (1, 4, 130, 1024, 16), (1, 8, 4096, 4096, 40),
+    # d = 40's pipelined loop: one ragged tile, exactly one / two / three whole tiles, a ragged third
+    (1, 8, 100, 20, 40), (1, 4, 70, 64, 40), (1, 4, 200, 128, 40), (2, 4, 70, 192, 40), (1, 4, 257, 150, 40),
 ])
 def test_attention(ops, B, H, nq, nk, d):
     from oracle.unet_ref import attention_core
@@ -251,10 +253,11 @@ def test_attention_causal(ops, B, H, n, d):
     assert rel_l2(o, ref) < 3e-3
 
 
-def test_attention_large_logits_rescale(ops):
+@pytest.mark.parametrize("d", [64, 40])
+def test_attention_large_logits_rescale(ops, d):
     """Force the online-softmax max to jump in a late key tile (rule: test the rescale branch)."""
     from oracle.unet_ref import attention_core
-    B, H, n, d = 1, 2, 256, 64
+    B, H, n = 1, 2, 256
     q = _rand(B, n, H, d, seed=12)
     k = _rand(B, n, H, d, seed=13)
     k[:, 200] = q[:, 5] * 4           # spike: row 5's max arrives in tile 3

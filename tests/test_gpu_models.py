@@ -1,9 +1,9 @@
 """Model-level parity on the MI355X (run with -m gpu): the HIP-backed mirrors against
 (a) the reference's own outputs (golden fixtures) at tiny sizes and (b) the CPU
 oracle at the real SD-1.x / VAE shapes.  Tolerance: fp16 activations, fp32
-accumulation and softmax; full-size models vs the fp32 oracle: rel-L2 <= 5e-3 and max-abs <= 2e-2 of the
-range (gpu_util.check_parity, ~3x the measured errors); tiny models vs the reference's golden outputs as
-stated per test."""
+accumulation and softmax; full-size models vs the fp32 oracle: rel-L2 and max-abs (of the range) limits stated
+per test at ~3-3.5x the errors measured on MI355X (gpu_util.check_parity, profiles/r5_parity_errors.txt); tiny
+models vs the reference's golden outputs as stated per test."""
 import json
 
 import numpy as np
@@ -97,7 +97,9 @@ def test_full_unet_vs_oracle(sdk, cfg_name, hw, ctx_dim):
     y = m(x.to(DEV), t.to(DEV), ctx.to(DEV) if ctx is not None else None)
     torch.set_num_threads(16)
     ref = unet_forward(sd, cfg, x, t, ctx)
-    check_parity(f"{cfg_name} full UNet", y, ref)
+    # limits ~3x the measured (rel-L2, max-abs): SD1 1.52e-3 / 1.55e-3, UNCOND 1.72e-3 / 1.80e-3, SD2 1.30e-3 / 1.31e-3
+    lim = {"SD1": (5e-3, 5e-3), "UNCOND": (5e-3, 6e-3), "SD2": (4.5e-3, 4.5e-3)}[cfg_name]
+    check_parity(f"{cfg_name} full UNet", y, ref, *lim)
 
 
 def test_full_vae_decode_vs_oracle(sdk):
@@ -117,7 +119,7 @@ def test_full_vae_decode_vs_oracle(sdk):
     dec = vae.decode(z.to(DEV), pre_scale=1.0 / 0.18215)
     torch.set_num_threads(16)
     ref = decode_first_stage(sd, dd, z, 0.18215)
-    check_parity("VAE decoder 64->512", dec, ref)
+    check_parity("VAE decoder 64->512", dec, ref, 3.5e-3, 3.5e-3)   # 1.07e-3 / 1.12e-3
 
 
 # ---------------------------------------------------------------- img2img
@@ -227,7 +229,7 @@ def test_full_vae_encode_vs_oracle(sdk):
     torch.set_num_threads(16)
     ref = autoencoder_moments(sd, dd, x)
     assert post.parameters.shape == (1, 8, 64, 64)
-    check_parity("VAE encoder 512->64 moments", post.parameters, ref)
+    check_parity("VAE encoder 512->64 moments", post.parameters, ref, 3.5e-3, 4e-3)   # 1.09e-3 / 1.25e-3
 
 
 # ---------------------------------------------------------------- CLIP text encoder
@@ -260,7 +262,7 @@ def test_full_clip_vit_l14_vs_oracle(sdk):
     y = m(ids)
     ref = clip_text_forward(sd, ids, 12)
     assert y.shape == (2, 77, 768)
-    check_parity("CLIP ViT-L/14 text tower", y, ref)
+    check_parity("CLIP ViT-L/14 text tower", y, ref, 3.5e-3, 6e-3)   # 1.09e-3 / 1.94e-3
 
 
 # ---------------------------------------------------------------- tiled decode
