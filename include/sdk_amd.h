@@ -116,12 +116,6 @@ typedef struct {
                               many M-panels, N-tile major inside a group, so the tiles co-resident on one XCD
                               share both their A panels and their W tiles in its L2; 0: the library's choice,
                               1: M-panel major (every N-tile of a panel, then the next panel) */
-  double* gn_group_stats;  /* NULL, or (with gn_partial) [batch][gn_groups] (mean, variance) pairs of the output's
-                              GroupNorm groups, merged INSIDE the launch by the last work item of each image to
-                              store its partials — sdk_group_norm_groups then normalises without a finalize */
-  uint32_t* gn_group_counters;  /* with gn_group_stats: >= batch zero-initialised words (device memory; every
-                                   launch leaves them zero) */
-  int32_t gn_groups;       /* with gn_group_stats: the consumer's groups (cout % gn_groups == 0, cout <= 1280) */
 } sdk_conv_args;
 
 #define SDK_TILE_COUNTERS 16384
@@ -194,13 +188,6 @@ int sdk_group_norm(const sdk_group_norm_args* a, int32_t silu, void* y, int32_t 
  * so the normalised tensor is never written. */
 int sdk_group_norm_finalize(const sdk_group_norm_args* a, const float* part0, int32_t nch0, const float* part1,
                             int32_t nch1, sdk_stream_t stream);
-
-/* GroupNorm (+ SiLU) from per-group statistics its producer merged in its own launch
- * (sdk_conv_args.gn_group_stats: [batch][groups] (mean, variance) doubles): one apply launch, no finalize.
- * y = silu?(x*scale + shift) into y [batch][h+2*pad][w+2*pad][ld_y] (pad 0: contiguous); one source
- * (a->c_split == a->channels); scale / shift / workspace of `a` unused. */
-int sdk_group_norm_groups(const sdk_group_norm_args* a, int32_t silu, void* y, int32_t ld_y, int32_t h, int32_t w,
-                          int32_t pad, const double* group_stats, sdk_stream_t stream);
 
 /* The post-activation GroupNorm of the DDPM (config C1) UNet (DDPM/models/layers.py:23-38 ConvBlock,
  * :311-338 ResNetBlock, :154 attention post-norm): y = [silu](x*scale + shift) + post_bias[b][c]

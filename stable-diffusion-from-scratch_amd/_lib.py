@@ -30,8 +30,7 @@ class ConvArgs(C.Structure):
                 ("residual", vp), ("res_ld", i32), ("out", vp), ("out_ld", i32), ("out_mode", i32),
                 ("split_k", i32), ("workspace", vp), ("workspace_bytes", i64), ("variant_hint", i32),
                 ("act", i32), ("gn_partial", vp), ("weight_batch_stride", i64), ("split_inlaunch", i32),
-                ("tile_counters", vp), ("tile_group_m", i32), ("gn_group_stats", vp), ("gn_group_counters", vp),
-                ("gn_groups", i32)]
+                ("tile_counters", vp), ("tile_group_m", i32)]
 
 
 class ConvPlanInfo(C.Structure):
@@ -82,7 +81,7 @@ class DdimArgs(C.Structure):
 OUT_NHWC_F16, OUT_NCHW_F32, OUT_GEGLU_F16, OUT_ROWS_F32 = 0, 1, 2, 3
 ACT_NONE, ACT_QUICK_GELU = 0, 1
 
-EXPORTS = ["sdk_conv2d_plan", "sdk_conv2d", "sdk_group_norm_workspace", "sdk_group_norm_affine", "sdk_group_norm_apply", "sdk_group_norm_apply_padded", "sdk_group_norm_apply_ex", "sdk_group_norm", "sdk_group_norm_finalize", "sdk_group_norm_groups", "sdk_layer_norm",
+EXPORTS = ["sdk_conv2d_plan", "sdk_conv2d", "sdk_group_norm_workspace", "sdk_group_norm_affine", "sdk_group_norm_apply", "sdk_group_norm_apply_padded", "sdk_group_norm_apply_ex", "sdk_group_norm", "sdk_group_norm_finalize", "sdk_layer_norm",
            "sdk_attention", "sdk_cross_attention_block_supported", "sdk_cross_attention_block", "sdk_cross_attention_block_ln", "sdk_segment_softmax", "sdk_ff_supported", "sdk_ff_packed_bytes", "sdk_ff_pack", "sdk_feed_forward", "sdk_token_linear_supported", "sdk_token_linear", "sdk_token_linear_ln", "sdk_ddim_step", "sdk_ddpm_step", "sdk_timestep_embedding", "sdk_nchw_to_nhwc",
            "sdk_diag_gaussian_sample", "sdk_stochastic_encode", "sdk_token_embedding", "sdk_extract_patches",
            "sdk_fold_patches", "sdk_upsample_bilinear2x", "sdk_upsample_nearest2x_padded", "sdk_gelu", "sdk_last_error", "sdk_version", "sdk_kernel_name",
@@ -112,7 +111,6 @@ def lib():
     L.sdk_group_norm_apply_ex.argtypes = [C.POINTER(GroupNormArgs), i32, vp, i32, vp, i32, vp, i32, vp]
     L.sdk_group_norm.argtypes = [C.POINTER(GroupNormArgs), i32, vp, i32, i32, i32, i32, vp, i32, vp, i32, vp]
     L.sdk_group_norm_finalize.argtypes = [C.POINTER(GroupNormArgs), vp, i32, vp, i32, vp]
-    L.sdk_group_norm_groups.argtypes = [C.POINTER(GroupNormArgs), i32, vp, i32, i32, i32, i32, vp, vp]
     L.sdk_upsample_bilinear2x.argtypes = [vp, vp, i32, i32, i32, i32, vp]
     L.sdk_upsample_nearest2x_padded.argtypes = [vp, i32, vp, i32, i32, i32, i32, i32, vp]
     L.sdk_gelu.argtypes = [vp, vp, i64, vp]

@@ -74,12 +74,6 @@ struct Params {
                         // the LDS-DMA A gather is a lane base + a scalar tap offset, no masks
   float2* gnp;          // GroupNorm statistics of the fp16 output: [batch][gn_nch][N] (mean, M2) over
   int gn_nch;           // hw_out / gn_nch rows each (one chunk = one M-tile, or 64 rows of the split-K reduce)
-  // with gnp: the image's last arriving work item merges its partials into per-group (mean, variance)
-  // (gn_group_tail): gng [batch][gn_groups], gncnt = per-image arrival counters (left zero), gn_arrivals =
-  // work items that store partials of one image
-  double2* gng;
-  unsigned* gncnt;
-  int gn_groups, gn_arrivals;
   // in-launch split-K (LDS-DMA tile kernels, split == 2): the K halves of a tile combine inside the launch;
   // partial = one fp32 accumulator blob per (tile, half), tcnt = per-tile arrival counters (left zero)
   int inl;
@@ -639,75 +633,6 @@ __device__ __forceinline__ void gn_tile_store(const Params& p, int m0, int n0, F
     }
   const int b0 = m0 / p.hw_out, chunk = (m0 - b0 * p.hw_out) / TBM;
   p.gnp[((size_t)b0 * p.gn_nch + chunk) * p.N + n0 + t] = r;
-}
-
-// The image's group statistics from its producer, in the producer's own launch.  Every work item that
-// stored GroupNorm partials of image b takes a ticket on the image's arrival counter (its waves' partial
-// stores drained, an agent-scope release — the in-launch split-K's publish pattern); the LAST arrival
-// acquires and merges the image's [gn_nch][N] partials in double, in gn_apply_part_kernel's order (per
-// channel: mean of the equal-count chunk means, sum of M2 + rows * sum (mean_k - mean)^2; per group:
-// mean of the channel means, sum of M2_c + hw * sum (mean_c - mean_g)^2), writes (mean, variance) per
-// group to gng[b] and re-arms the counter.  The consumer's GroupNorm then runs no finalize launch
-// (sdk_group_norm_groups).  `scratch`: >= 16 * N bytes of idle LDS (N <= SDK_GN_TAIL_MAXN).
-constexpr int SDK_GN_TAIL_MAXN = 1280;
-
-__device__ __forceinline__ double gn_wave_sum_d(double v) {
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
-
-__device__ __forceinline__ void gn_group_tail(const Params& p, int b, void* scratch) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  unsigned* flag = reinterpret_cast<unsigned*>(scratch);
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = __hip_atomic_fetch_add(p.gncnt + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned last = t + 1 == (unsigned)p.gn_arrivals ? 1u : 0u;
-    if (last) {
-      __hip_atomic_store(p.gncnt + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // left zero
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    *flag = last;
-  }
-  __syncthreads();
-  const bool last = *flag != 0;
-  __syncthreads();   // every wave read the flag before the scratch is reused
-  if (!last) return;
-  double2* cs = reinterpret_cast<double2*>(scratch);   // [N] per-channel (mean, M2)
-  const int nch = p.gn_nch, N = p.N;
-  const double rows = (double)p.hw_out / nch;
-  const float2* part = p.gnp + (size_t)b * nch * N;
-  for (int c = threadIdx.x; c < N; c += blockDim.x) {
-    double ms = 0.0;
-    for (int k = 0; k < nch; ++k) ms += (double)part[(size_t)k * N + c].x;
-    const double mean = ms / nch;
-    double m2 = 0.0, dd = 0.0;
-    for (int k = 0; k < nch; ++k) {
-      const float2 q = part[(size_t)k * N + c];
-      const double dl = (double)q.x - mean;
-      m2 += (double)q.y;
-      dd += dl * dl;
-    }
-    cs[c] = make_double2(mean, m2 + rows * dd);
-  }
-  __syncthreads();
-  const int G = p.gn_groups, cg = N / G, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
-  for (int g = threadIdx.x >> 6; g < G; g += nw) {
-    double ms = 0.0;
-    for (int ci = lane; ci < cg; ci += 64) ms += cs[g * cg + ci].x;
-    ms = gn_wave_sum_d(ms);
-    const double mg = ms / cg;
-    double m2g = 0.0;
-    for (int ci = lane; ci < cg; ci += 64) {
-      const double dm = cs[g * cg + ci].x - mg;
-      m2g += cs[g * cg + ci].y + (double)p.hw_out * dm * dm;
-    }
-    m2g = gn_wave_sum_d(m2g);
-    if (lane == 0) p.gng[(size_t)b * G + g] = make_double2(mg, (m2g > 0 ? m2g : 0.0) / ((double)p.hw_out * cg));
-  }
 }
 
 // split-K reduce: a lane's pivot-shifted sums over its rows (registers are plentiful there)
@@ -1731,7 +1656,6 @@ __global__ void __launch_bounds__(CF::NT, CF::OCC * CF::NW / 4) conv_glds_kernel
     __syncthreads();
     gn_tile_store<CF::WM, CF::WN, CF::TN, CF::TM / BR, BR, CF::TBM, CF::TBN>(
         p, m0, n0, [&](int w) { return reinterpret_cast<const float2*>(lds + w * WSCR + scratch_halfs); });
-    if (p.gng) gn_group_tail(p, m0 / p.hw_out, lds);
   };
   if constexpr (CF::M16) {
     if (lds_epi && p.gnp) {
@@ -2219,7 +2143,6 @@ __global__ void __launch_bounds__(512) conv_ph_kernel(Params p) {
         const int vm = w >> 2, wn = w & 3;   // virtual wave row = 2 * half + wr
         return reinterpret_cast<const float2*>(lds + ((vm >> 1) * 8 + (vm & 1) * 4 + wn) * PWS + EPI_BYTES / 2);
       });
-      if (p.gng) gn_group_tail(p, m0 / p.hw_out, lds);
       return;
     }
     epilogue_lds<2, 2>(p, acc[0], m0, n0, wr * 64, wc * 64, lds + wave * (EPI_BYTES / 2), bias_s, rb_s);
@@ -2363,9 +2286,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(Params p) {
 // (hw_out / gn_nch rows of one image); per-lane pivot-shifted sums, Chan merge of the 32 row lanes
 // through LDS, one (mean, M2) per chunk and channel.
 __global__ void __launch_bounds__(256) splitk_reduce_gn_kernel(Params p) {
-  __shared__ double2 sbuf[SDK_GN_TAIL_MAXN];   // the row-lane partials, then gn_group_tail's scratch
-  static_assert(sizeof(sbuf) >= 32 * 64 * sizeof(float2), "row-lane partials fit");
-  float2 (*red)[64] = reinterpret_cast<float2 (*)[64]>(sbuf);
+  __shared__ float2 red[32][64];
   const int tc = threadIdx.x & 7, tr = threadIdx.x >> 3;
   const int b = blockIdx.x / p.gn_nch, chunk = blockIdx.x - b * p.gn_nch;
   const int R = p.hw_out / p.gn_nch;
@@ -2408,20 +2329,18 @@ __global__ void __launch_bounds__(256) splitk_reduce_gn_kernel(Params p) {
   }
   __syncthreads();
   const int c = threadIdx.x, nn = blockIdx.y * 64 + c;
-  if (c < 64 && nn < p.N) {
-    float2 acc = red[0][c];
-    float na = (float)((R + 31) / 32);
-    for (int t = 1; t < 32 && t < R; ++t) {
-      const float nb = (float)((R - t + 31) / 32);
-      const float2 q = red[t][c];
-      const float dl = q.x - acc.x, f = nb / (na + nb);
-      acc.x += dl * f;
-      acc.y += q.y + dl * dl * na * f;
-      na += nb;
-    }
-    p.gnp[((size_t)b * p.gn_nch + chunk) * p.N + nn] = acc;
+  if (c >= 64 || nn >= p.N) return;
+  float2 acc = red[0][c];
+  float na = (float)((R + 31) / 32);
+  for (int t = 1; t < 32 && t < R; ++t) {
+    const float nb = (float)((R - t + 31) / 32);
+    const float2 q = red[t][c];
+    const float dl = q.x - acc.x, f = nb / (na + nb);
+    acc.x += dl * f;
+    acc.y += q.y + dl * dl * na * f;
+    na += nb;
   }
-  if (p.gng) gn_group_tail(p, b, sbuf);
+  p.gnp[((size_t)b * p.gn_nch + chunk) * p.N + nn] = acc;
 }
 
 // Direct convolution for a handful of output channels (variant 34): the UNet's conv_out (320 -> 4)
@@ -3028,17 +2947,6 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
       return fail(SDK_EINVAL, "conv2d: this plan emits no GroupNorm statistics (sdk_conv_plan_info.gn_chunks == 0)");
     p.gnp = reinterpret_cast<float2*>(a->gn_partial);
     p.gn_nch = gn_nch;
-  }
-  if (a->gn_group_stats) {
-    if (!p.gnp) return fail(SDK_EINVAL, "conv2d: gn_group_stats needs gn_partial");
-    if (a->gn_groups <= 0 || p.N % a->gn_groups || p.N > SDK_GN_TAIL_MAXN || !a->gn_group_counters)
-      return fail(SDK_EINVAL, "conv2d: gn_group_stats needs gn_groups dividing cout <= 1280 and gn_group_counters");
-    p.gng = reinterpret_cast<double2*>(a->gn_group_stats);
-    p.gncnt = a->gn_group_counters;
-    p.gn_groups = a->gn_groups;
-    // work items storing one image's partials: the split-K reduce's (chunk, 64-column block) items, or the
-    // tiles of the image (M-tiles inside it x N-tiles; the in-launch split's combining tiles)
-    p.gn_arrivals = (split > 1 && !p.inl) ? gn_nch * ((p.N + 63) / 64) : gn_nch * p.tiles_n;
   }
   return SDK_OK;
 }

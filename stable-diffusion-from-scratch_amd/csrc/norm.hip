@@ -644,68 +644,6 @@ __global__ void __launch_bounds__(256) gn_apply_pad_row_kernel(const half_t* s0,
   }
 }
 
-// GroupNorm apply from per-group statistics (sdk_group_norm_groups: [batch][groups] (mean, variance) doubles that
-// the producing conv merged in its own launch, sdk_conv_args.gn_group_stats): grid (row splits, image); each
-// workgroup turns its image's group statistics into per-channel scale / shift in LDS (the finalize's formulas:
-// rstd = 1/sqrt(var + eps) in double, shift = beta - mean * scale) and normalises (+ SiLU) a contiguous range of
-// the (optionally zero-bordered) image's 8-channel vectors, GNP_U loads in flight per thread.
-__global__ void __launch_bounds__(256) gn_apply_groups_kernel(const half_t* x, int ldx, int h, int w, int pad,
-                                                              int channels, int groups, const double2* gs, float eps,
-                                                              const float* gamma, const float* beta, int silu,
-                                                              half_t* y, int ldy, int per_split) {
-  extern __shared__ __attribute__((aligned(16))) float gst[];   // [channels] scale | [channels] shift
-  const int tid = threadIdx.x, b = blockIdx.y;
-  const int cg = channels / groups, c8 = channels / 8, hp = h + 2 * pad, wp = w + 2 * pad;
-  for (int c = tid; c < channels; c += 256) {
-    const double2 st = gs[(size_t)b * groups + c / cg];
-    const float rstd = (float)(1.0 / sqrt(st.y + (double)eps));
-    const float meanf = (float)st.x;
-    const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
-    const float sc = gm * rstd;
-    gst[c] = sc;
-    gst[channels + c] = bt - meanf * sc;
-  }
-  __syncthreads();
-  const int total = hp * wp * c8;
-  const int e0 = blockIdx.x * per_split, e1 = min(total, e0 + per_split);
-  const half_t* xb = x + (size_t)b * h * w * ldx;
-  half_t* yb = y + (size_t)b * hp * wp * ldy;
-  for (int i0 = e0 + tid; i0 < e1; i0 += 256 * GNP_U) {
-    h8 v[GNP_U];
-    int pp[GNP_U], cc[GNP_U];
-    bool in[GNP_U];
-#pragma unroll
-    for (int u = 0; u < GNP_U; ++u) {
-      const int i = i0 + 256 * u;
-      pp[u] = i / c8;
-      cc[u] = (i - pp[u] * c8) * 8;
-      const int py = pp[u] / wp, px = pp[u] - py * wp;
-      const int iy = py - pad, ix = px - pad;
-      in[u] = i < e1 && (unsigned)iy < (unsigned)h && (unsigned)ix < (unsigned)w;
-      v[u] = in[u] ? *reinterpret_cast<const h8*>(xb + ((size_t)iy * w + ix) * ldx + cc[u]) : h8{};
-    }
-#pragma unroll
-    for (int u = 0; u < GNP_U; ++u) {
-      if (i0 + 256 * u >= e1) break;
-      h8 o = {};
-      if (in[u]) {
-        const f4* ps = reinterpret_cast<const f4*>(gst + cc[u]);
-        const f4* pt = reinterpret_cast<const f4*>(gst + channels + cc[u]);
-        const f4 sa = ps[0], sb = ps[1], ta = pt[0], tb = pt[1];
-        const float sc[8] = {sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3]};
-        const float sh[8] = {ta[0], ta[1], ta[2], ta[3], tb[0], tb[1], tb[2], tb[3]};
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          float t = (float)v[u][j] * sc[j] + sh[j];
-          if (silu) t = t * __builtin_amdgcn_rcpf(1.0f + __expf(-t));
-          o[j] = (half_t)t;
-        }
-      }
-      *reinterpret_cast<h8*>(yb + (size_t)pp[u] * ldy + cc[u]) = o;
-    }
-  }
-}
-
 // Nearest-x2 upsample into a zero-bordered image (UNet Upsample, reference openai_model/model.py:120-131:
 // F.interpolate(scale_factor=2, mode="nearest") then the 3x3 conv with padding 1): y[b][py][px] =
 // x[b][(py - pad) >> 1][(px - pad) >> 1] inside, 0 on the border — the conv then runs unmasked (pad 0) on the
@@ -1100,30 +1038,6 @@ extern "C" int sdk_group_norm(const sdk_group_norm_args* a, int32_t silu, void* 
   }
   return pad ? sdk_group_norm_apply_padded(a, silu, y, ld_y, h, w, pad, stream)
              : sdk_group_norm_apply(a, silu, y, ld_y, stream);
-}
-
-extern "C" int sdk_group_norm_groups(const sdk_group_norm_args* a, int32_t silu, void* y, int32_t ld_y, int32_t h,
-                                     int32_t w, int32_t pad, const double* group_stats, sdk_stream_t stream) {
-  if (!a || !a->src0 || !y || !group_stats) return fail(SDK_EINVAL, "group_norm_groups: null pointer");
-  if (a->channels % 8 || a->groups <= 0 || a->channels % a->groups || ld_y % 8 || ld_y < a->channels ||
-      a->ld0 % 8 || a->ld0 < a->channels)
-    return fail(SDK_EINVAL, "group_norm_groups: channels/ld must be multiples of 8, channels % groups == 0");
-  if (a->c_split != a->channels) return fail(SDK_EINVAL, "group_norm_groups: one source (c_split == channels)");
-  if (h <= 0 || w <= 0 || (int64_t)h * w != a->hw || pad < 0 || pad > 4)
-    return fail(SDK_EINVAL, "group_norm_groups: h*w must equal hw, pad in [0, 4]");
-  const int64_t total = (int64_t)(h + 2 * pad) * (w + 2 * pad) * (a->channels / 8);
-  if (total >= (1ll << 31) || a->channels > 4096 || a->batch > 65535)
-    return fail(SDK_EINVAL, "group_norm_groups: image too large");
-  if (a->batch <= 0) return SDK_OK;
-  // ~8 vectors per thread per workgroup, at least ~1024 workgroups when the image allows
-  int64_t splits = std::max<int64_t>(1, (total + 2047) / 2048);
-  splits = std::max<int64_t>(splits, std::min<int64_t>((1024 + a->batch - 1) / a->batch, (total + 255) / 256));
-  const int per = (int)((total + splits - 1) / splits);
-  const int grid = (int)((total + per - 1) / per);
-  hipLaunchKernelGGL(gn_apply_groups_kernel, dim3(grid, a->batch), dim3(256), (size_t)a->channels * 8,
-                     (hipStream_t)stream, (const half_t*)a->src0, a->ld0, h, w, pad, a->channels, a->groups,
-                     (const double2*)group_stats, a->eps, a->gamma, a->beta, silu, (half_t*)y, ld_y, per);
-  return check_launch("gn_apply_groups");
 }
 
 extern "C" int sdk_upsample_nearest2x_padded(const void* x, int32_t ld_x, void* y, int32_t batch, int32_t h, int32_t w,

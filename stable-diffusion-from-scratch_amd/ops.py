@@ -82,18 +82,6 @@ class _Workspace:
             self.buf[key] = c
         return c
 
-    def gn_counters(self, device) -> torch.Tensor:
-        """Per-image arrival counters of the GroupNorm group-statistics tail (sdk_conv_args.gn_group_counters):
-        zeroed once, left zero by every launch (the image's last arrival resets its word)."""
-        key = (torch.device(device).index, self.lane, "gncnt")
-        c = self.buf.get(key)
-        if c is None:
-            if torch.cuda.is_current_stream_capturing():
-                raise RuntimeError("sd_amd: GroupNorm counters must exist before graph capture (run one warm-up step)")
-            c = torch.zeros(GN_TAIL_MAX_BATCH, dtype=torch.int32, device=device)
-            self.buf[key] = c
-        return c
-
     def get(self, nbytes: int, device) -> torch.Tensor:
         key = (torch.device(device).index, self.lane)
         b = self.buf.get(key)
@@ -110,7 +98,6 @@ class _Workspace:
 
 WORKSPACE = _Workspace()
 TILE_COUNTERS = 16384     # sdk_amd.h SDK_TILE_COUNTERS
-GN_TAIL_MAX_BATCH = 4096  # images per conv launch whose GroupNorm group statistics the producer merges
 
 
 # --------------------------------------------------------------------------- sources
@@ -384,21 +371,14 @@ TILE_GROUP_M = None
 # GroupNorm statistics emitted by the producing conv (tensor attribute; see conv2d(gn_stats=True))
 GN_ATTR = "_sd_gn_partial"
 EMIT_GN_STATS = True      # tests / A/B: False = every GroupNorm runs its own statistics pass
-# per-group (mean, variance) merged inside the producing conv's launch (sdk_conv_args.gn_group_stats) for a
-# GroupNorm of GN_TAIL_GROUPS groups: the consumer then runs one apply launch, no finalize (tensor attribute)
-GN_GROUPS_ATTR = "_sd_gn_groups"
-GN_TAIL_GROUPS = 32
-GN_GROUP_TAIL = __import__("os").environ.get("SD_AMD_GN_GROUP_TAIL", "1") != "0"   # A/B: 0 = partials only
 
 
 def _claim(out):
     """A caller-supplied ``out`` is about to be overwritten through the C ABI, which does not move
     torch's version counter: drop any GroupNorm statistics a previous producer attached to it, so
     only the plan that writes it now can attach (fresh) ones."""
-    if out is not None:
-        for attr in (GN_ATTR, GN_GROUPS_ATTR):
-            if hasattr(out, attr):
-                delattr(out, attr)
+    if out is not None and hasattr(out, GN_ATTR):
+        delattr(out, GN_ATTR)
     return out
 
 
@@ -444,9 +424,6 @@ def _conv2d_batch_chunks(pc, x, seg2, gn, row_bias, residual, out, B, kw):
     parts = [getattr(o, GN_ATTR, None) for o in outs]
     if all(pp is not None for pp in parts) and len({pp[1] for pp in parts}) == 1:
         setattr(full, GN_ATTR, (torch.cat([pp[0] for pp in parts], 0), parts[0][1], full._version))
-    gg = [getattr(o, GN_GROUPS_ATTR, None) for o in outs]
-    if all(g is not None for g in gg):
-        setattr(full, GN_GROUPS_ATTR, (torch.cat([g[0] for g in gg], 0), gg[0][1], full._version))
     return full
 
 
@@ -543,15 +520,10 @@ def conv2d(pc: PackedConv, x, *, ksize=None, stride=1, pad=None, pad_end=0, upsa
         ws = WORKSPACE.get(info.workspace_bytes, dev)
         a.workspace = ws.data_ptr()
         a.workspace_bytes = ws.numel()
-    part = gstats = None
+    part = None
     if want_gn and info.gn_chunks > 0 and out.shape[-1] == pc.N:
         part = torch.empty(B, info.gn_chunks, pc.N, 2, dtype=torch.float32, device=dev)
         a.gn_partial = part.data_ptr()
-        if GN_GROUP_TAIL and pc.N % GN_TAIL_GROUPS == 0 and pc.N <= 1280 and B <= GN_TAIL_MAX_BATCH:
-            gstats = torch.empty(B, GN_TAIL_GROUPS, 2, dtype=torch.float64, device=dev)
-            a.gn_group_stats = gstats.data_ptr()
-            a.gn_group_counters = WORKSPACE.gn_counters(dev).data_ptr()
-            a.gn_groups = GN_TAIL_GROUPS
     if PROFILER.active:
         # algorithmic HBM bytes: each source tensor, the weights and the output once (+ residual)
         nb = sum(t.numel() * 2 for t in _as_pair(x) if t is not None) + pc.N * pc.k_total * 2
@@ -566,8 +538,6 @@ def conv2d(pc: PackedConv, x, *, ksize=None, stride=1, pad=None, pad_end=0, upsa
         # the statistics describe `out` as written now: group_norm ignores them once the tensor has
         # been modified in place (its version counter moved)
         setattr(out, GN_ATTR, (part, info.gn_chunks, out._version))
-    if gstats is not None:
-        setattr(out, GN_GROUPS_ATTR, (gstats, GN_TAIL_GROUPS, out._version))
     return out
 
 
@@ -785,16 +755,6 @@ def group_norm(x, gamma, beta, eps, groups=32, silu=True, pad=0, out=None):
                                                           device=dev)
     # statistics the producing convs emitted (every source must carry them)
     srcs = [t for t in _as_pair(x) if t is not None]
-    gg = getattr(srcs[0], GN_GROUPS_ATTR, None) if len(srcs) == 1 else None
-    if gg is not None and gg[1] == groups and gg[2] == srcs[0]._version:
-        # the producer merged the group statistics in its own launch: one apply launch
-        if PROFILER.active:
-            PROFILER.begin("group_norm", None)
-        check(lib().sdk_group_norm_groups(C.byref(args), 1 if silu else 0, _ptr(y), y.shape[-1], H, W, pad,
-                                          _ptr(gg[0]), _stream()), "group_norm_groups")
-        if PROFILER.active:
-            PROFILER.end()
-        return y
     parts = [getattr(t, GN_ATTR, None) for t in srcs]
     parts = [pp if pp is not None and pp[2] == t._version else None for pp, t in zip(parts, srcs)]
     p0 = p1 = None

@@ -82,8 +82,6 @@ def main():
         nch = max(1, H * H // 256)
         part = torch.zeros(B, nch, C, 2, device="cuda")
         part[..., 1] = H * H / nch
-        gst = torch.zeros(B, 32, 2, dtype=torch.float64, device="cuda")
-        gst[..., 1] = 1.0
         y = torch.empty(B, H + 2, H + 2, C, dtype=torch.float16, device="cuda")
         nb = x.numel() * 2 + y.numel() * 2
 
@@ -92,13 +90,7 @@ def main():
             ops.group_norm(x, g, b, 1e-5, 32, silu=True, pad=1, out=y)
             delattr(x, ops.GN_ATTR)
 
-        def from_groups():
-            setattr(x, ops.GN_GROUPS_ATTR, (gst, 32, x._version))
-            ops.group_norm(x, g, b, 1e-5, 32, silu=True, pad=1, out=y)
-            delattr(x, ops.GN_GROUPS_ATTR)
-
         row("GN+SiLU from partials", f"{B}x{H}x{H}x{C}", nb, timeit(from_parts), ceil)
-        row("GN+SiLU from groups", f"{B}x{H}x{H}x{C}", nb, timeit(from_groups), ceil)
     for M, C in ((16384, 640), (4096, 1280), (1024, 1280)):
         x = torch.randn(M, C, device="cuda").half()
         g, b = torch.ones(C, device="cuda"), torch.zeros(C, device="cuda")
