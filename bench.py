@@ -488,7 +488,7 @@ def main():
             ach = conv["flops"] / conv["launches"] / avg_s / 1e12
             out["roofline"] = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
                                "frac": round(ach / PEAK_F16_TFLOPS, 4), "traffic": pmc_traffic(args),
-                               "kernel": "conv family: conv_glds_kernel / conv_ph_kernel / conv_halo_kernel / "
+                               "kernel": "conv family: conv_glds_kernel / conv_ph_kernel / "
                                          "conv_igemm_kernel / conv_direct_kernel / conv_skinny_kernel "
                                          "(+splitk_reduce_kernel on split-K launches)",
                                "launches": conv["launches"], "avg_launch_us": round(1e6 * avg_s, 2),

@@ -17,7 +17,7 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CONV = ("conv_glds_kernel", "conv_ph_kernel", "conv_halo_kernel", "conv_igemm_kernel", "conv_direct_kernel",
+CONV = ("conv_glds_kernel", "conv_ph_kernel", "conv_igemm_kernel", "conv_direct_kernel",
         "conv_skinny_kernel", "splitk_reduce_kernel", "splitk_reduce_gn_kernel")
 
 
