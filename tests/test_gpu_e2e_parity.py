@@ -38,7 +38,7 @@ def max_abs_rel(a, b):
 
 def _report(tag, got, ref, rl2_max, mabs_max):
     rl2, mab = rel_l2(got, ref), max_abs_rel(got, ref)
-    print(f"[parity] {tag}: rel-L2 {rl2:.3e} (<= {rl2_max:.0e})  max-abs/max {mab:.3e} (<= {mabs_max:.0e})",
+    print(f"[parity] {tag}: rel-L2 {rl2:.3e} (<= {rl2_max:.1e})  max-abs/max {mab:.3e} (<= {mabs_max:.1e})",
           flush=True)
     assert rl2 <= rl2_max, f"{tag}: rel-L2 {rl2:.3e}"
     assert mab <= mabs_max, f"{tag}: max-abs {mab:.3e}"
