@@ -46,8 +46,14 @@ class Upsample(nn.Module):
         self._pc = ops.PackedConv([(self.conv.weight, self.in_channels)], self.conv.bias, device=dev)
 
     def _run(self, x):
-        # the output feeds the next ResnetBlock's norm1: the conv emits its GroupNorm statistics
-        return ops.conv2d(self._pc, x, upsample=True, gn_stats=True)
+        # the output feeds the next ResnetBlock's norm1: the conv emits its GroupNorm statistics.  As in the UNet's
+        # Upsample (openai_model/model.py), the nearest-x2 image is written zero-bordered and the 3x3 conv runs
+        # unmasked with pad 0 on the linear A issue, instead of folding the upsample into every DMA address
+        # (the folded form ran the 512^2 decoder convs at 730-830 TF/s); SD_AMD_UPSAMPLE_FOLD=1 restores it
+        from ..openai_model.model import UPSAMPLE_FOLD
+        if UPSAMPLE_FOLD or x.shape[-1] % 8:
+            return ops.conv2d(self._pc, x, upsample=True, gn_stats=True)
+        return ops.conv2d(self._pc, ops.upsample_nearest2x_padded(x, 1), pad=0, gn_stats=True)
 
 
 class Downsample(nn.Module):
