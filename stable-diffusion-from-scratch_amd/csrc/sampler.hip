@@ -385,8 +385,6 @@ extern "C" const char* sdk_kernel_name(int32_t variant) {
     case 33: return "conv_glds_kernel<Cfg<128,160,4,1,4,m16>>";
     case 34: return "conv_direct_kernel";
     case 35: return "conv_skinny_kernel";
-    case 36: return "conv_halo_kernel<HCfg<256,320,8,2>>";
-    case 37: return "conv_halo_kernel<HCfg<128,320,4,2>>";
     default: return "unknown";
   }
 }

@@ -79,6 +79,7 @@ def test_conv_plan_picks_skinny_and_names_every_variant(sdk):
     assert L.sdk_conv2d_plan(C.byref(a), C.byref(info)) != 0         # forced 35 on 65 rows
     a.variant_hint = 37                                # the retired halo-tile ids 36 / 37 are unknown
     assert L.sdk_conv2d_plan(C.byref(a), C.byref(info)) != 0
+    assert L.sdk_kernel_name(36) == b"unknown" and L.sdk_kernel_name(37) == b"unknown"
     a.variant_hint = 39
     assert L.sdk_conv2d_plan(C.byref(a), C.byref(info)) != 0         # unknown id
 
