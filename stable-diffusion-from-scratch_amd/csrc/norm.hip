@@ -588,6 +588,56 @@ __global__ void __launch_bounds__(256) gn_apply_pad_kernel(const half_t* s0, con
   }
 }
 
+// The same transform (padded or not), one pass: each thread owns GNA_U vectors of the output spaced 256 apart (every
+// load of the thread issued before the first store), 32-bit element indices split by host-verified multiply-shift
+// reciprocals (pad_row_divm) instead of the 64-bit divisions of the grid-stride forms — those cost more VALU than
+// the byte moving at the 64x64 / 32x32 levels.  e -> (padded pixel, 8-channel chunk) -> (image, padded row, column).
+constexpr int GNA_U = 4;
+__global__ void __launch_bounds__(256) gn_apply_flat_kernel(const half_t* s0, const half_t* s1, int c_split, int ld0,
+                                                            int ld1, int h, int w, int pad, int channels,
+                                                            const float* scale, const float* shift, int silu,
+                                                            half_t* y, int ldy, unsigned nvec, unsigned m_c8,
+                                                            unsigned m_img, unsigned m_wp) {
+  const unsigned c8 = (unsigned)channels / 8, hp = h + 2 * pad, wp = w + 2 * pad, npix = hp * wp;
+  const unsigned e0 = blockIdx.x * (256u * GNA_U) + threadIdx.x;
+  h8 v[GNA_U];
+  unsigned ppix[GNA_U], cc[GNA_U], bb[GNA_U];
+  bool in[GNA_U];
+#pragma unroll
+  for (int u = 0; u < GNA_U; ++u) {
+    const unsigned e = e0 + 256u * u;
+    const unsigned p = (unsigned)(((unsigned long long)e * m_c8) >> 32);           // e / c8
+    const unsigned b = (unsigned)(((unsigned long long)p * m_img) >> 32);          // p / npix
+    const unsigned r = p - b * npix;
+    const unsigned ry = (unsigned)(((unsigned long long)r * m_wp) >> 32);          // r / wp
+    const int iy = (int)ry - pad, ix = (int)(r - ry * wp) - pad;
+    ppix[u] = p;
+    cc[u] = (e - p * c8) * 8;
+    bb[u] = b;
+    in[u] = e < nvec && (unsigned)iy < (unsigned)h && (unsigned)ix < (unsigned)w;
+    v[u] = in[u] ? load_px(s0, s1, c_split, ld0, ld1, ((size_t)b * h + iy) * w + ix, (int)cc[u]) : h8{};
+  }
+#pragma unroll
+  for (int u = 0; u < GNA_U; ++u) {
+    if (e0 + 256u * u >= nvec) break;
+    h8 o = {};
+    if (in[u]) {
+      const f4* ps = reinterpret_cast<const f4*>(scale + (size_t)bb[u] * channels + cc[u]);
+      const f4* pt = reinterpret_cast<const f4*>(shift + (size_t)bb[u] * channels + cc[u]);
+      const f4 sa = ps[0], sb = ps[1], ta = pt[0], tb = pt[1];
+      const float sc[8] = {sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3]};
+      const float sh[8] = {ta[0], ta[1], ta[2], ta[3], tb[0], tb[1], tb[2], tb[3]};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float x = (float)v[u][j] * sc[j] + sh[j];
+        if (silu) x = x * __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+        o[j] = (half_t)x;
+      }
+    }
+    *reinterpret_cast<h8*>(y + (size_t)ppix[u] * ldy + cc[u]) = o;
+  }
+}
+
 // The same per padded row: grid (padded row, image); the image's scale / shift staged in LDS once, the row's
 // (pixel, 8-channel chunk) elements split by a host-verified multiply-shift (no 64-bit index division per
 // element), GNP_U loads in flight per thread.  Same arithmetic per element (profiles/r4_gn_apply_pad_ab.txt).
@@ -858,6 +908,31 @@ extern "C" int sdk_group_norm_affine(const sdk_group_norm_args* a, sdk_stream_t 
   return check_launch("gn_finalize");
 }
 
+// SDK_GN_APPLY_FLAT: 1 (default) = gn_apply_flat_kernel below 128x128 pixels, 2 = everywhere, 0 = the grid-stride /
+// row forms only (A/B)
+static const int g_gn_apply_flat = [] {
+  const char* e = getenv("SDK_GN_APPLY_FLAT");
+  return e ? atoi(e) : 1;
+}();
+
+// the one-pass apply when its reciprocals are exact over every index it forms (tail lanes included); 1 = launched
+static int gn_apply_flat(const sdk_group_norm_args* a, int silu, void* y, int ld_y, int h, int w, int pad,
+                         hipStream_t s) {
+  if (g_gn_apply_flat == 0 || (g_gn_apply_flat == 1 && (int64_t)h * w >= 128 * 128)) return 0;
+  const int64_t npix = (int64_t)(h + 2 * pad) * (w + 2 * pad), c8 = a->channels / 8;
+  const int64_t nvec = (int64_t)a->batch * npix * c8, span = nvec + 256 * GNA_U;
+  if (span >= (1LL << 31) || npix >= (1 << 30)) return 0;
+  const unsigned m_c8 = c8 > 1 ? pad_row_divm((int)span, (int)c8) : 0u;
+  const unsigned m_img = npix > 1 ? pad_row_divm((int)(span / c8 + 1), (int)npix) : 0u;
+  const unsigned m_wp = (w + 2 * pad) > 1 ? pad_row_divm((int)npix, w + 2 * pad) : 0u;
+  if (!m_c8 || !m_img || !m_wp) return 0;
+  const unsigned blocks = (unsigned)((nvec + 256 * GNA_U - 1) / (256 * GNA_U));
+  hipLaunchKernelGGL(gn_apply_flat_kernel, dim3(blocks), dim3(256), 0, s, (const half_t*)a->src0,
+                     (const half_t*)a->src1, a->c_split, a->ld0, a->ld1, h, w, pad, a->channels, a->scale, a->shift,
+                     silu, (half_t*)y, ld_y, (unsigned)nvec, m_c8, m_img, m_wp);
+  return 1;
+}
+
 extern "C" int sdk_group_norm_apply(const sdk_group_norm_args* a, int32_t silu, void* y, int32_t ld_y,
                                     sdk_stream_t stream) {
   if (!a || !a->src0 || !a->scale || !a->shift || !y) return fail(SDK_EINVAL, "group_norm_apply: null pointer");
@@ -867,6 +942,8 @@ extern "C" int sdk_group_norm_apply(const sdk_group_norm_args* a, int32_t silu, 
   if (a->c_split < a->channels && !a->src1) return fail(SDK_EINVAL, "group_norm_apply: concat without src1");
   const int64_t nvec = (int64_t)a->batch * a->hw * (a->channels / 8);
   if (nvec <= 0) return SDK_OK;
+  if (a->hw < (1 << 30) && gn_apply_flat(a, silu, y, ld_y, 1, (int)a->hw, 0, (hipStream_t)stream))
+    return check_launch("gn_apply_flat");
   const int blocks = (int)std::min<int64_t>((nvec + 255) / 256, 8192);
   hipLaunchKernelGGL(gn_apply_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const half_t*)a->src0,
                      (const half_t*)a->src1, a->c_split, a->ld0, a->ld1, a->hw, a->channels, a->scale, a->shift,
@@ -886,6 +963,7 @@ extern "C" int sdk_group_norm_apply_padded(const sdk_group_norm_args* a, int32_t
   const int64_t nvec = (int64_t)a->batch * (h + 2 * pad) * (w + 2 * pad) * (a->channels / 8);
   if (nvec <= 0) return SDK_OK;
   const int hp = h + 2 * pad, wp = w + 2 * pad;
+  if (gn_apply_flat(a, silu, y, ld_y, h, w, pad, (hipStream_t)stream)) return check_launch("gn_apply_flat");
   const unsigned divm = (int64_t)wp * (a->channels / 8) < (1 << 24) ? pad_row_divm(wp * (a->channels / 8), a->channels / 8) : 0;
   // the row form where it measured faster (the VAE decoder's >= 128x128 images: 206.6 -> 182.5 us at 128x128x512,
   // 696.6 -> 677.8 at 512x512x128); the grid-stride form elsewhere (64x64x640 56.6 vs 58.9 us, 16x16 17.4 vs 19.4)
