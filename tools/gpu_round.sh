@@ -31,10 +31,12 @@ fi
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
   step tests 1100 python -u -m pytest tests -m gpu -v -s --timeout 400 --timeout-method thread
 fi
-step bench_c3 600 env BENCH_SHAPES_OUT=$O/shapes.txt python -u bench.py --steps 5 --warmup 2
-step bench_c5 600 python -u bench.py --config c5 --steps 2 --warmup 1
-step bench_c2 600 python -u bench.py --config c2 --steps 3 --warmup 1
-step bench_c1 600 python -u bench.py --config c1 --steps 5 --warmup 2
+if [ "${SKIP_BENCH:-0}" != "1" ]; then
+  step bench_c3 600 env BENCH_SHAPES_OUT=$O/shapes.txt python -u bench.py --steps 5 --warmup 2
+  step bench_c5 600 python -u bench.py --config c5 --steps 2 --warmup 1
+  step bench_c2 600 python -u bench.py --config c2 --steps 3 --warmup 1
+  step bench_c1 600 python -u bench.py --config c1 --steps 5 --warmup 2
+fi
 if [ "${SKIP_PROF:-0}" != "1" ]; then
   cd /tmp
   step trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline
