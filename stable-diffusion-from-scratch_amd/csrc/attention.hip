@@ -424,10 +424,11 @@ extern "C" int sdk_attention(const sdk_attention_args* a, sdk_stream_t stream) {
   // d = 160 keeps 4 waves: at 256 query rows one 8-wave group per head would idle half the CUs
   static const int nw4 = getenv("SDK_ATTN_NW") && atoi(getenv("SDK_ATTN_NW")) == 4;
   // SDK_ATTN_STAG=1: the 8-wave forms with the lag half staggered by half a tile (three stages).  Default on
-  // for 48 < d <= 64 only (same-box A/B, profiles/r3_attn_stag_ab.txt: d = 64 975 vs 1060 us at SD-2's 96x96
-  // level, d = 40 582 vs 521 us); SDK_ATTN_STAG=0 / 1 forces it off / on everywhere
+  // for 48 < d <= 80 (same-box A/Bs: d = 64 975 vs 1060 us at SD-2's 96x96 level, d = 40 582 vs 521 us,
+  // profiles/r3_attn_stag_ab.txt; d = 80 at SD-1's 32x32 level 67.1-67.5 vs 69.3 us, profiles/r5_attn80_ab.txt);
+  // SDK_ATTN_STAG=0 / 1 forces it off / on everywhere
   static const int stag_env = getenv("SDK_ATTN_STAG") ? atoi(getenv("SDK_ATTN_STAG")) : -1;
-  const int stag = stag_env == 1 || (stag_env < 0 && d > 48 && d <= 64);
+  const int stag = stag_env == 1 || (stag_env < 0 && d > 48 && d <= 80);
   if (d <= 48)
     return qb2 ? launch<48, 64, 4, 2>(p, s)
            : nw4  ? launch<48, 64, 4, 1>(p, s)
