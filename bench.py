@@ -99,10 +99,47 @@ def build_models(cfg, device, graph=False):
     return unet, vae, ld
 
 
-def make_one_step(sampler, ld, xT, ctx, ddim_steps, world, gathered):
+class GatherTimer:
+    """Device time of the all-gather of each step: HIP events on the current stream around the
+    collective (all_gather_into_tensor makes the current stream wait for RCCL's stream, so the closing
+    event completes after the collective); wall clock on the CPU (gloo is synchronous there)."""
+
+    def __init__(self, device):
+        self.cuda = device.type == "cuda"
+        self.reset()
+
+    def reset(self):
+        self.marks = []
+
+    def run(self, fn):
+        if self.cuda:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            out = fn()
+            e1.record()
+            self.marks.append((e0, e1))
+        else:
+            t0 = time.perf_counter()
+            out = fn()
+            self.marks.append(1000.0 * (time.perf_counter() - t0))
+        return out
+
+    def mean_ms(self):
+        if not self.marks:
+            return None
+        if self.cuda:
+            torch.cuda.synchronize()
+            ms = [a.elapsed_time(b) for a, b in self.marks]
+        else:
+            ms = self.marks
+        return sum(ms) / len(ms)
+
+
+def make_one_step(sampler, ld, xT, ctx, ddim_steps, world, gathered, gather_timer=None):
     """One bench step on one rank: 50-step DDIM over the rank's shard (x_T and context already in
     HBM), the VAE decode, and — for N > 1 ranks — the one collective of the path, an all-gather of
-    the decoded images into ``gathered`` (rank-major, all_gather_into_tensor: RCCL over xGMI)."""
+    the decoded images into ``gathered`` (rank-major, all_gather_into_tensor: RCCL over xGMI), timed by
+    ``gather_timer`` when given."""
     from sd_amd import distributed as sdd
     B, shape = xT.shape[0], tuple(xT.shape[1:])
 
@@ -111,24 +148,45 @@ def make_one_step(sampler, ld, xT, ctx, ddim_steps, world, gathered):
                               verbose=False, log_every_t=10 ** 9)
         img = ld.decode_first_stage(z)
         if world > 1:
-            sdd.gather(img.half(), world, out=gathered)
+            gat = lambda: sdd.gather(img.half(), world, out=gathered)   # noqa: E731
+            gather_timer.run(gat) if gather_timer is not None else gat()
         return img
     return one_step
 
 
-def timed_steps(one_step, steps, warmup, barrier, device):
+def timed_steps(one_step, steps, warmup, barrier, device, gather_timer=None):
     """W untimed warm-up steps, then exactly K steps between barrier + synchronize pairs; the
-    elapsed time is the MAX over ranks."""
+    elapsed time is the MAX over ranks.  ``gather_timer`` keeps the timed steps' all-gathers only."""
     from sd_amd import distributed as sdd
     img = None
     for _ in range(warmup):
         img = one_step()
     barrier()
+    if gather_timer is not None:
+        gather_timer.reset()
     t0 = time.perf_counter()
     for _ in range(steps):
         img = one_step()
     barrier()
     return img, sdd.max_over_ranks(time.perf_counter() - t0, device=device)
+
+
+def dp_report(img, gathered, rank, world, device, gather_timer):
+    """Evidence of the N-rank run, for the bench line (every rank calls it: it holds collectives):
+    the world size and backend the process group reports, the mean device time of the timed steps'
+    all-gathers (max over ranks), and a bitwise check that slice r of the gathered batch is rank r's own
+    fp16 image batch of the last step (mismatching ranks counted by an all-reduce)."""
+    import torch.distributed as tdist
+    from sd_amd import distributed as sdd
+    B = img.shape[0]
+    ok = torch.equal(gathered[rank * B:(rank + 1) * B], img.half())
+    bad = torch.tensor([0 if ok else 1], dtype=torch.int64, device=device)
+    tdist.all_reduce(bad, op=tdist.ReduceOp.SUM)
+    ag = gather_timer.mean_ms() if gather_timer is not None else None
+    return {"ranks_seen": tdist.get_world_size(), "backend": tdist.get_backend(),
+            "allgather_ms": None if ag is None else round(sdd.max_over_ranks(ag, device=device), 3),
+            "allgather_bytes_per_rank": img[:1].numel() * B * 2,
+            "gather_slices_bitwise_equal": int(bad.item()) == 0, "gather_mismatched_ranks": int(bad.item())}
 
 
 def make_barrier(dist, device):
@@ -417,7 +475,8 @@ def main():
 
     xT, ctx = rank_inputs(2024, world, rank, B, (4, L, L), cfg["ctx"], device)
     gathered = torch.empty(world * B, 3, 8 * L, 8 * L, dtype=torch.float16, device=device) if dist else None
-    one_step = make_one_step(sampler, model, xT, ctx, args.ddim_steps, world, gathered)
+    gtimer = GatherTimer(device) if dist else None
+    one_step = make_one_step(sampler, model, xT, ctx, args.ddim_steps, world, gathered, gtimer)
     barrier = make_barrier(dist, device)
 
     # the first warm-up step (eager) also autotunes every distinct conv problem missing from the
@@ -434,8 +493,9 @@ def main():
     model.use_graphs(not args.no_graph)
     if not args.no_graph:                # capture the UNet graph (setup, not a sampling step)
         model.apply_model(xT, torch.full((B,), 999, dtype=torch.long, device=device), ctx)
-    img, elapsed = timed_steps(one_step, args.steps, max(args.warmup - 1, 0), barrier, device)
+    img, elapsed = timed_steps(one_step, args.steps, max(args.warmup - 1, 0), barrier, device, gtimer)
     finite = bool(torch.isfinite(img).all().item())
+    dp = dp_report(img, gathered, rank, world, device, gtimer) if dist else None
 
     # UNet step latency at the config batch (HIP events around replays of the sampler's UNet call,
     # through apply_model -> DiffusionWrapper -> graph replay)
@@ -476,6 +536,8 @@ def main():
                                "decode_first_stage"},
            "unet_step_ms": round(unet_ms, 3), "finite": finite, "hip_graph": not args.no_graph,
            "autotuned_conv_problems": len(ops.AUTOTUNE.table), "tuning_cache_entries": cached}
+    if dp is not None:
+        out.update(dp)
     if not args.no_roofline and rank == 0:
         summ = ops.PROFILER.summary()
         conv = {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0}

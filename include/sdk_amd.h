@@ -184,8 +184,9 @@ int sdk_group_norm(const sdk_group_norm_args* a, int32_t silu, void* y, int32_t 
 /* The statistics half of sdk_group_norm alone: a->scale / a->shift [batch][channels] of the
  * GroupNorm affine, merged from the producers' per-chunk statistics (part0 / part1 as above) or, with
  * none, computed from x (sdk_group_norm_affine).  For a conv that applies GroupNorm + SiLU to its own
- * A operand (sdk_conv_src.gn_scale / gn_shift / silu: the transform-prologue plans, variants 0 / 35),
- * so the normalised tensor is never written. */
+ * A operand (sdk_conv_src.gn_scale / gn_shift / silu), so the normalised tensor is never written: only
+ * variant 0, the register-staged kernel, takes the GroupNorm scale / shift prologue; variant 35 (skinny)
+ * is planned only without gn_scale and applies SiLU alone. */
 int sdk_group_norm_finalize(const sdk_group_norm_args* a, const float* part0, int32_t nch0, const float* part1,
                             int32_t nch1, sdk_stream_t stream);
 

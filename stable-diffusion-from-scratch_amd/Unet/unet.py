@@ -50,10 +50,17 @@ class Upsample(nn.Module):
         # Upsample (openai_model/model.py), the nearest-x2 image is written zero-bordered and the 3x3 conv runs
         # unmasked with pad 0 on the linear A issue, instead of folding the upsample into every DMA address
         # (the folded form ran the 512^2 decoder convs at 730-830 TF/s); SD_AMD_UPSAMPLE_FOLD=1 restores it
+        # The materialised image is a temporary of B·(2H+2)·(2W+2)·C·2 bytes beside the input and the output: at C5
+        # (B = 8, 384 -> 768, 256 channels) 2.4 GB; above UPSAMPLE_MATERIALISE_MAX_BYTES the folded form runs instead
         from ..openai_model.model import UPSAMPLE_FOLD
-        if UPSAMPLE_FOLD or x.shape[-1] % 8:
+        n, h, w, c = x.shape
+        big = n * (2 * h + 2) * (2 * w + 2) * c * 2 > UPSAMPLE_MATERIALISE_MAX_BYTES
+        if UPSAMPLE_FOLD or c % 8 or big:
             return ops.conv2d(self._pc, x, upsample=True, gn_stats=True)
         return ops.conv2d(self._pc, ops.upsample_nearest2x_padded(x, 1), pad=0, gn_stats=True)
+
+
+UPSAMPLE_MATERIALISE_MAX_BYTES = 8 << 30   # the VAE Upsample's zero-bordered x2 image
 
 
 class Downsample(nn.Module):

@@ -13,7 +13,7 @@ LIB = os.path.join(HERE, "libsdk_amd.so")
 SOURCES = ["conv.hip", "norm.hip", "attention.hip", "sampler.hip", "xattn.hip", "ff.hip", "token.hip", "probe.hip"]
 # conv.hip is compiled once per part (its SDK_CONV_PART partition: host planner + small kernels, then the tile
 # kernel instantiations in four groups) so the objects build in parallel
-CONV_PARTS = 5
+CONV_PARTS = 6
 
 
 def _units():
@@ -105,6 +105,13 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False, tag: s
                 for name, u in usage:
                     f.write(f"{name} vgpr={u.get('VGPRs')} agpr={u.get('AGPRs')} scratch={u.get('ScratchSize')} "
                             f"occ={u.get('Occupancy')}\n")
+            if os.path.basename(obj).startswith("token") and not any(
+                    NO_SCRATCH.search(n) and "ScratchSize" in u for n, u in usage):
+                # the check below must see the kernel: missing or reformatted remarks fail the build
+                # rather than pass it silently (profiles/r6_resource_usage.txt is a parsed sample)
+                os.remove(obj)
+                raise RuntimeError("no kernel-resource-usage remark for token_linear320_kernel: cannot verify "
+                                   "that it uses no scratch")
             bad = [n for n, u in usage if NO_SCRATCH.search(n) and u.get("ScratchSize", 0) > 0]
             for n, u in usage:
                 if WARN_SCRATCH.search(n) and u.get("ScratchSize", 0) > 0:

@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <string>
 #include <type_traits>
+#include <cstdio>
 #include <cstdlib>
 
 #include "common.h"
@@ -1277,6 +1278,7 @@ __global__ void __launch_bounds__(CF::NT, CF::OCC * CF::NW / 4) conv_glds_kernel
   constexpr int GPW = CF::GPW;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  __builtin_assume(wave >= 0 && wave < CF::NW);   // lets the piece loops resolve real / A / W pieces at compile time
   const int wm = wave / CF::WN, wn = wave % CF::WN;
   const int nitems = p.tiles_m * p.tiles_n * p.split;
   // XCD-aware item order: neighbouring tiles (shared A rows / W rows) share an L2
@@ -1422,6 +1424,13 @@ __global__ void __launch_bounds__(CF::NT, CF::OCC * CF::NW / 4) conv_glds_kernel
     int toff, woff;
     bool live, s1, sec;
   };
+  // A/B builds only (-DSDK_ABL_DMA=1 / 2 / 3, wrong outputs by design): the K loop issues no A / W / A and W
+  // pieces after the prologue — the ablations that say which operand's fill bounds the loop
+#if defined(SDK_ABL_DMA)
+#define SDK_ABL_DMA_SKIP(IS_A) (((SDK_ABL_DMA) & 1) && (IS_A)) || (((SDK_ABL_DMA) & 2) && !(IS_A))
+#else
+#define SDK_ABL_DMA_SKIP(IS_A) false
+#endif
   auto stage_prep = [&](int KT) __attribute__((always_inline)) {
     Iss q;
     q.live = KT < kt1;
@@ -1442,18 +1451,21 @@ __global__ void __launch_bounds__(CF::NT, CF::OCC * CF::NW / 4) conv_glds_kernel
   };
   // piece J (a compile-time index after unrolling: the per-lane offset arrays stay in registers) of the
   // stage described by Q into ring slot BUF
+// Branch-free: a padding piece (piece >= NINSTR, every wave issues GPW so the vmcnt immediates are exact) differs
+// from a real one only in its operands — its per-lane offset is PH_OOB (cx set up so) and it lands in the dummy slot
+// past the ring — so the K-step stays one basic block and the scheduler can hoist the fragment reads across the
+// DMA issue (a uniform branch per piece split the unrolled K-step into ~12 blocks, each B fragment read right before
+// its MFMAs)
 #define SDK_PIECE(Q, J, BUF)                                                                             \
   do {                                                                                                   \
     const int piece_ = (J) * CF::NW + wave;                                                              \
-    if (piece_ >= CF::NINSTR) {                                                                          \
-      ph_dma(d.w, lds + CF::NS * CF::STAGE_H, PH_OOB, 0);                                                \
-    } else {                                                                                             \
-      const bool a_ = piece_ * 8 < CF::TBM;                                                              \
-      unsigned base_ = cx[J];                                                                            \
-      if constexpr (SIMPLE == 2) base_ = (a_ && (Q).s1) ? ((Q).sec ? cz[J] : cy[J]) : cx[J];             \
-      ph_dma(a_ ? (Q).ra : d.w, lds + (BUF) * CF::STAGE_H + piece_ * 8 * BK, (Q).live ? base_ : PH_OOB,  \
-             a_ ? (Q).toff : (Q).woff);                                                                  \
-    }                                                                                                    \
+    const bool real_ = piece_ < CF::NINSTR;                                                              \
+    const bool a_ = piece_ * 8 < CF::TBM;                                                                \
+    if (real_ && SDK_ABL_DMA_SKIP(a_)) break;                                                            \
+    unsigned base_ = cx[J];                                                                              \
+    if constexpr (SIMPLE == 2) base_ = (a_ && (Q).s1) ? ((Q).sec ? cz[J] : cy[J]) : cx[J];               \
+    ph_dma(a_ ? (Q).ra : d.w, real_ ? lds + (BUF) * CF::STAGE_H + piece_ * 8 * BK : lds + CF::NS * CF::STAGE_H, \
+           (Q).live ? base_ : PH_OOB, a_ ? (Q).toff : (Q).woff);                                         \
   } while (0)
   for (int kt = kt0; kt < kt1; ++kt) {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"((CF::NS - 2) * GPW) : "memory");
@@ -1468,29 +1480,58 @@ __global__ void __launch_bounds__(CF::NT, CF::OCC * CF::NW / 4) conv_glds_kernel
     }
     const half_t* st = lds + buf * CF::STAGE_H;
     if constexpr (CF::M16) {
+      // the K-step as G = (BK / 32) x FN16 MFMA groups (group g: W fragment j = g % FN16 of K half kk = g / FN16
+      // against the wave's FM16 A fragments).  PFD > 0 (the 8-wave configs, 256 VGPRs): every A fragment of the
+      // K-step is read up front and W fragments run PFD groups ahead of their MFMAs, so an LDS read's latency
+      // hides under the MFMAs of the groups before it; PFD = 0 (16 waves at 128 VGPRs): one W fragment at a time
+      // (the 32x160 wave tiles keep 80 accumulator VGPRs), A fragments per K half
+      constexpr int G = (BK / 32) * CF::FN16;
+      constexpr int PFD = CF::NW * CF::OCC <= 8 ? 2 : 0;
+      constexpr int NKA = PFD ? BK / 32 : 1;
+      auto rd_b = [&](int g) __attribute__((always_inline)) {
+        return *reinterpret_cast<const h8*>(st + swz(brow16 + (g % CF::FN16) * 16, (g / CF::FN16) * 4 + c16));
+      };
+      h8 fa[NKA][CF::FM16];
+      h8 fbq[PFD + 1];
+      if constexpr (PFD > 0) {
 #pragma unroll
-      for (int kk = 0; kk < BK / 32; ++kk) {
-        h8 fa[CF::FM16];
-#pragma unroll
-        for (int i = 0; i < CF::FM16; ++i)
-          fa[i] = *reinterpret_cast<const h8*>(st + swz(arow16 + i * 16, kk * 4 + c16));
-        // one W fragment at a time: the 32x160 wave tiles of the 16-wave configs keep
-        // 80 accumulator VGPRs and must stay within 128
-#pragma unroll
-        for (int j = 0; j < CF::FN16; ++j) {
-          const h8 fb = *reinterpret_cast<const h8*>(st + swz(brow16 + j * 16, kk * 4 + c16));
+        for (int kk = 0; kk < BK / 32; ++kk)
 #pragma unroll
           for (int i = 0; i < CF::FM16; ++i)
-            acc16[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb, fa[i], acc16[i][j], 0, 0, 0);
-          // pieces [g * PPG, (g + 1) * PPG) after MFMA group g: all issued within the first half of the
-          // K-step's groups, so they land while the rest of it computes
-          const int g = kk * CF::FN16 + j;
-          if constexpr (SIMPLE != 0) {
-            constexpr int PPG = (2 * GPW + CF::FN16 * (BK / 32) - 1) / (CF::FN16 * (BK / 32));
+            fa[kk][i] = *reinterpret_cast<const h8*>(st + swz(arow16 + i * 16, kk * 4 + c16));
 #pragma unroll
-            for (int r = 0; r < PPG; ++r)
-              if (g * PPG + r < GPW) SDK_PIECE(q, g * PPG + r < GPW ? g * PPG + r : 0, wbuf);
+        for (int g = 0; g < PFD; ++g) fbq[g] = rd_b(g);
+      }
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const int kk = g / CF::FN16, j = g % CF::FN16;
+        if constexpr (PFD == 0) {
+          if (j == 0) {
+#pragma unroll
+            for (int i = 0; i < CF::FM16; ++i)
+              fa[0][i] = *reinterpret_cast<const h8*>(st + swz(arow16 + i * 16, kk * 4 + c16));
           }
+        }
+        const h8 fb = PFD ? fbq[g % (PFD + 1)] : rd_b(g);
+        if constexpr (PFD > 0) {
+          if (g + PFD < G) fbq[(g + PFD) % (PFD + 1)] = rd_b(g + PFD);
+        }
+#pragma unroll
+        for (int i = 0; i < CF::FM16; ++i) {
+          const h8 fai = fa[PFD ? kk : 0][i];
+#if defined(SDK_ABL_MFMA)   // A/B builds only: the fragments are consumed by one VALU add instead of the MFMA
+          acc16[i][j][0] += (float)fb[0] + (float)fai[0];
+#else
+          acc16[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb, fai, acc16[i][j], 0, 0, 0);
+#endif
+        }
+        // pieces [g * PPG, (g + 1) * PPG) after MFMA group g: all issued within the first half of the
+        // K-step's groups, so they land while the rest of it computes
+        if constexpr (SIMPLE != 0) {
+          constexpr int PPG = (2 * GPW + G - 1) / G;
+#pragma unroll
+          for (int r = 0; r < PPG; ++r)
+            if (g * PPG + r < GPW) SDK_PIECE(q, g * PPG + r < GPW ? g * PPG + r : 0, wbuf);
         }
       }
     } else {
@@ -1704,6 +1745,13 @@ using Cfg128x128r3m = Cfg<128, 128, 2, 2, 3, true>;
 using Cfg128x160o2m = Cfg<128, 160, 4, 1, 2, true, 2>;
 using Cfg128x128o2m = Cfg<128, 128, 2, 2, 2, true, 2>;
 using Cfg128x160r4m = Cfg<128, 160, 4, 1, 4, true>;      // one workgroup, 3 K-steps of DMA in flight
+// 8-wave 256-row tiles with 64-row (256x320) / 128-row (256x256) wave tiles at two waves per SIMD (256 VGPRs): half
+// the LDS fragment reads per MFMA of the 16-wave 256x320 (each B fragment feeds 4 or 8 MFMAs instead of 2) and room
+// for the fragment reads of the next group to be in flight under the current one's MFMAs (round-6 ablation, profiles/
+// r6_conv_ablation.txt: the 16-wave 256x320 runs at 1.16 PF/s with no DMA at all — its LDS-read -> MFMA chain, not
+// the fill, bounds it)
+using Cfg256x320w8m = Cfg<256, 320, 4, 2, 2, true>;
+using Cfg256x256w8m = Cfg<256, 256, 2, 4, 2, true>;
 
 // ---------------------------------------------------------------------- 16x16x32 epilogues
 // Transposed 16x16 accumulator (D^T = W A^T, v_mfma_f32_16x16x32_f16): lane l holds pixel
@@ -2577,12 +2625,19 @@ int launch_glds(const Params& p, hipStream_t s) {
 #define SDK_HIDDEN __attribute__((visibility("hidden")))
 }  // namespace
 }  // namespace sdk
-extern "C" SDK_HIDDEN int sdk_conv_launch_part1(int v, const void* pp, void* st);
-extern "C" SDK_HIDDEN int sdk_conv_launch_part2(int v, const void* pp, void* st);
-extern "C" SDK_HIDDEN int sdk_conv_launch_part3(int v, const void* pp, void* st);
-extern "C" SDK_HIDDEN int sdk_conv_launch_part4(int v, const void* pp, void* st);
-#define SDK_PART_FN(k) extern "C" SDK_HIDDEN int sdk_conv_launch_part##k(int v, const void* pp, void* st) { \
+extern "C" SDK_HIDDEN int sdk_conv_launch_part1(int v, const void* pp, int psize, void* st);
+extern "C" SDK_HIDDEN int sdk_conv_launch_part2(int v, const void* pp, int psize, void* st);
+extern "C" SDK_HIDDEN int sdk_conv_launch_part3(int v, const void* pp, int psize, void* st);
+extern "C" SDK_HIDDEN int sdk_conv_launch_part4(int v, const void* pp, int psize, void* st);
+extern "C" SDK_HIDDEN int sdk_conv_launch_part5(int v, const void* pp, int psize, void* st);
+// Params lives in an anonymous namespace, so each part compiles its own copy of the type: the caller passes
+// its sizeof(Params) and a part whose layout differs (a part-only preprocessor state) refuses the launch
+#define SDK_PART_FN(k) extern "C" SDK_HIDDEN int sdk_conv_launch_part##k(int v, const void* pp, int psize,       \
+                                                                    void* st) {                           \
     using namespace sdk;                                                                                \
+    if (psize != (int)sizeof(Params))                                                                   \
+      return fail(SDK_EINVAL, "conv2d: Params layout differs between compile parts (" +                 \
+                                  std::to_string(psize) + " vs " + std::to_string(sizeof(Params)) + ")"); \
     const Params& p = *static_cast<const Params*>(pp);                                                 \
     const hipStream_t s = (hipStream_t)st;                                                              \
     switch (v) {
@@ -2617,6 +2672,12 @@ SDK_PART_FN(3)
     case 31: return launch_glds<Cfg128x160o2m>(p, s);
     case 32: return launch_glds<Cfg128x128o2m>(p, s);
     case 33: return launch_glds<Cfg128x160r4m>(p, s);
+SDK_PART_END
+#endif
+#if SDK_PART(5)
+SDK_PART_FN(5)
+    case 38: return launch_glds<Cfg256x320w8m>(p, s);
+    case 40: return launch_glds<Cfg256x256w8m>(p, s);
 SDK_PART_END
 #endif
 #if SDK_PART(4)
@@ -2795,7 +2856,7 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   }
   // forced configuration: the caller's autotuner (variant_hint = 1 + id) or, for
   // benchmarks, SDK_CONV_VARIANT=id (read once, at library load)
-  const int forced = a->variant_hint > 0 ? a->variant_hint - 1 : g_env_variant;
+  int forced = a->variant_hint > 0 ? a->variant_hint - 1 : g_env_variant;
   // variant 34: direct convolution for <= 8 output channels (conv_out of the UNet / VAE decoder)
   {
     const sdk_conv_src& g = a->seg[0];
@@ -2851,25 +2912,35 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   // ids: 0 register-staged; 2..7 LDS-DMA configs; 8, 9 phased 256x256; 10..15 diagnostics;
   // 16..19 deep-ring LDS-DMA configs; 20, 21 phased 256x256 on v_mfma_f32_16x16x32_f16;
   // 22..26 LDS-DMA configs 256x320, 7, 6, 19, 18 on v_mfma_f32_16x16x32_f16 (5 retired); 27..30 diagnostics;
-  // 31, 32 two-per-CU 128x160 / 128x128 (16x16x32); 33 128x160 with a 4-stage ring; 34 direct (<= 8 outputs).
+  // 31, 32 two-per-CU 128x160 / 128x128 (16x16x32); 33 128x160 with a 4-stage ring; 34 direct (<= 8 outputs);
+  // 38 8-wave 256x320, 40 8-wave 256x256 (16x16x32; 39, the 256x320 on 32x32x16, spilled and is not built).
   // The diagnostic ablations compute wrong outputs by design: the product library rejects them,
   // only the separate diagnostics build (-DSDK_CONV_DIAGNOSTICS, libsdk_amd_diag.so) runs them.
   if (is_diagnostic_variant(forced) && !kDiagnostics)
     return fail(SDK_EINVAL, "conv2d: variant " + std::to_string(forced) +
                                 " is a diagnostic ablation (only in libsdk_amd_diag.so)");
-  if (forced > 35 || forced == 1) return fail(SDK_EINVAL, "conv2d: unknown variant " + std::to_string(forced));
+  if (forced == 1 || (forced > 35 && forced < 38) || forced == 39 || forced > 40)
+    return fail(SDK_EINVAL, "conv2d: unknown variant " + std::to_string(forced));
   // variant 5 (256x320 on 32x32x16, 16 waves) spilled at the 128-VGPR cap of 4 waves per SIMD — scratch VMEM
-  // ops under hand-counted vmcnt waits; variant 22 is the same tile on 16x16x32 without spills
-  if (forced == 5) return fail(SDK_EINVAL, "conv2d: variant 5 is retired (use 22)");
+  // ops under hand-counted vmcnt waits; variant 22 is the same tile on 16x16x32 without spills, so a forced 5
+  // (a leftover SDK_CONV_VARIANT=5 or an old tuning entry) runs as 22, with a one-time warning
+  if (forced == 5) {
+    static std::atomic<bool> warned{false};
+    if (!warned.exchange(true))
+      fprintf(stderr, "sd_amd conv2d: variant 5 is retired; running the same 256x320 tile as variant 22\n");
+    forced = 22;
+  }
   const int fbase = forced;
-  const bool fvalid = forced >= 0 && forced != 1 && forced <= 33;
+  const bool fvalid = forced >= 0 && forced != 1 && (forced <= 33 || forced == 38 || forced == 40);
   const bool fgeglu = (fbase <= 4 || fbase >= 8) && fbase != 22 && fbase != 23 && fbase != 24 && fbase != 31 &&
-                      fbase != 33;
+                      fbase != 33 && fbase != 38;
   if (fvalid && (forced == 0 || !transform) && (fgeglu || a->out_mode != SDK_OUT_GEGLU_F16)) {
-    static const int fbm[34] = {128, 0, 256, 256, 128, 256, 256, 128, 256, 256, 256, 256, 256, 256, 256, 256, 128,
-                                256, 128, 128, 256, 256, 256, 128, 256, 128, 128, 256, 256, 256, 256, 128, 128, 128};
-    static const int fbn[34] = {128, 0, 256, 128, 128, 320, 160, 320, 256, 256, 256, 256, 256, 256, 256, 256, 128,
-                                128, 128, 256, 256, 256, 320, 320, 160, 256, 128, 256, 256, 256, 256, 160, 128, 160};
+    static const int fbm[41] = {128, 0, 256, 256, 128, 256, 256, 128, 256, 256, 256, 256, 256, 256, 256, 256, 128,
+                                256, 128, 128, 256, 256, 256, 128, 256, 128, 128, 256, 256, 256, 256, 128, 128, 128,
+                                0, 0, 0, 0, 256, 256, 256};
+    static const int fbn[41] = {128, 0, 256, 128, 128, 320, 160, 320, 256, 256, 256, 256, 256, 256, 256, 256, 128,
+                                128, 128, 256, 256, 256, 320, 320, 160, 256, 128, 256, 256, 256, 256, 160, 128, 160,
+                                0, 0, 0, 0, 320, 320, 256};
     if (!p.wbs || (forced != 0 && p.hw_out % fbm[fbase] == 0)) {
       var = forced;
       tbm = fbm[fbase];
@@ -2910,9 +2981,9 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   int64_t ws = split > 1 ? (int64_t)split * p.M * p.Npad * 4 : 0;
   if (a->split_inlaunch) {
     const bool tile_kernel = (var >= 2 && var <= 7) || (var >= 16 && var <= 19) || (var >= 22 && var <= 26) ||
-                             (var >= 31 && var <= 33);
+                             (var >= 31 && var <= 33) || var == 38 || var == 40;
     if (!tile_kernel)
-      return fail(SDK_EINVAL, "conv2d: in-launch split-K needs an LDS-DMA tile plan (variants 2-7, 16-19, 22-26, 31-33)");
+      return fail(SDK_EINVAL, "conv2d: in-launch split-K needs an LDS-DMA tile plan (variants 2-7, 16-19, 22-26, 31-33, 38, 40)");
     if (split != 2) return fail(SDK_EINVAL, "conv2d: in-launch split-K combines exactly two K halves (split_k = 2)");
     if (!a->tile_counters) return fail(SDK_EINVAL, "conv2d: in-launch split-K needs tile_counters");
     if (tiles > SDK_TILE_COUNTERS) return fail(SDK_EINVAL, "conv2d: in-launch split-K: more tiles than counters");
@@ -2935,7 +3006,7 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   // reduce kernel, 64-row chunks (one chunk when hw_out is not a multiple of 64); otherwise the
   // LDS-DMA kernels' fp16 epilogue, one chunk per M-tile when tiles do not straddle images.
   const bool glds = (var >= 2 && var <= 9) || (var >= 16 && var <= 19) || (var >= 22 && var <= 26) ||
-                    (var >= 31 && var <= 33);   // 8 / 9: the phased kernel's 32x32x16 epilogue
+                    (var >= 31 && var <= 33) || var == 38 || var == 40;   // 8 / 9: the phased kernel's 32x32x16 epilogue
   int gn_nch = 0;
   if (a->out_mode == SDK_OUT_NHWC_F16) {
     if (split > 1 && !p.inl) gn_nch = p.hw_out % 64 == 0 ? p.hw_out / 64 : 1;
@@ -2971,13 +3042,14 @@ extern "C" int sdk_conv2d(const sdk_conv_args* a, sdk_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
   dim3 grid(p.tiles_m * p.tiles_n, p.split);
   switch (p.variant) {
-    case 2: case 3: case 4: case 6: case 7: rc = sdk_conv_launch_part1(p.variant, &p, s); break;
-    case 16: case 17: case 18: case 19: case 22: case 23: rc = sdk_conv_launch_part2(p.variant, &p, s); break;
-    case 24: case 25: case 26: case 31: case 32: case 33: rc = sdk_conv_launch_part3(p.variant, &p, s); break;
+    case 2: case 3: case 4: case 6: case 7: rc = sdk_conv_launch_part1(p.variant, &p, (int)sizeof(Params), s); break;
+    case 16: case 17: case 18: case 19: case 22: case 23: rc = sdk_conv_launch_part2(p.variant, &p, (int)sizeof(Params), s); break;
+    case 24: case 25: case 26: case 31: case 32: case 33: rc = sdk_conv_launch_part3(p.variant, &p, (int)sizeof(Params), s); break;
     case 8: case 9: case 20: case 21: case 10: case 11: case 12: case 13: case 14: case 15: case 27: case 28:
     case 29: case 30:
-      rc = sdk_conv_launch_part4(p.variant, &p, s);
+      rc = sdk_conv_launch_part4(p.variant, &p, (int)sizeof(Params), s);
       break;
+    case 38: case 40: rc = sdk_conv_launch_part5(p.variant, &p, (int)sizeof(Params), s); break;
     case 34: rc = launch_direct(p, s); break;
     case 35: rc = launch_skinny(p, s); break;
     default:

@@ -385,6 +385,8 @@ extern "C" const char* sdk_kernel_name(int32_t variant) {
     case 33: return "conv_glds_kernel<Cfg<128,160,4,1,4,m16>>";
     case 34: return "conv_direct_kernel";
     case 35: return "conv_skinny_kernel";
+    case 38: return "conv_glds_kernel<Cfg<256,320,4,2,2,m16>>";
+    case 40: return "conv_glds_kernel<Cfg<256,256,2,4,2,m16>>";
     default: return "unknown";
   }
 }

@@ -233,7 +233,7 @@ class _Autotune:
     Enabled by ``enable()`` (UNetModel/AutoEncoderKL.prepare(autotune=True)); the
     first call of each distinct problem times every candidate (HIP events, 3 reps
     after a warm-up; SD_AMD_TUNE_REPS) and caches the fastest.  Never runs under graph capture."""
-    VARIANTS = (2, 7, 6, 4, 3, 8, 9, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 31, 32, 33, 34, 35)
+    VARIANTS = (2, 7, 6, 4, 3, 8, 9, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 31, 32, 33, 34, 35, 38, 40)
     # split -2: two K halves combined inside the launch (sdk_conv_args.split_inlaunch; LDS-DMA tile kernels)
     # (3 and 6: 80 256x256 tiles of a 16x16-level conv x 3 = 240 workgroups, one wave of the 256 CUs)
     SPLITS = (0, 1, 2, 3, 4, 6, 8, 12, 16, -2)

@@ -62,14 +62,21 @@ def _worker(rank, world, port, out_q):
         xT, ctx = bench.rank_inputs(2024, world, rank, B, (4, L, L), (5, 16), dev)
         assert xT.shape == (B, 4, L, L) and ctx.shape == (B, 5, 16)
         gathered = torch.empty(world * B, 3, 8 * L, 8 * L, dtype=torch.float16)
-        one_step = bench.make_one_step(_StubSampler(), _StubLD(), xT, ctx, 4, world, gathered)
+        gt = bench.GatherTimer(dev)
+        one_step = bench.make_one_step(_StubSampler(), _StubLD(), xT, ctx, 4, world, gathered, gt)
         barrier = bench.make_barrier(True, dev)
-        img, elapsed = bench.timed_steps(one_step, 2, 1, barrier, dev)
+        img, elapsed = bench.timed_steps(one_step, 2, 1, barrier, dev, gt)
         assert img.shape == (B, 3, 8 * L, 8 * L) and elapsed > 0
+        assert len(gt.marks) == 2          # the timed steps' gathers only (warm-up dropped)
+        dp = bench.dp_report(img, gathered, rank, world, dev, gt)
+        # a corrupted slice (rank 1's image in the gathered buffer) is caught on every rank
+        bad = gathered.clone()
+        bad[B + 1, 0, 0, 0] += 1
+        dp_bad = bench.dp_report(img, bad, rank, world, dev, gt)
         from sd_amd import distributed as sdd
         t = sdd.max_over_ranks(0.5 + rank)
         if rank == 0:
-            out_q.put((gathered, t))
+            out_q.put((gathered, t, dp, dp_bad))
     finally:
         dist.destroy_process_group()
 
@@ -84,7 +91,7 @@ def test_bench_dp_step_matches_single_process():
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    gathered, t = q.get(timeout=120)
+    gathered, t, dp, dp_bad = q.get(timeout=120)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -94,6 +101,12 @@ def test_bench_dp_step_matches_single_process():
     ref = _StubLD().decode_first_stage(z).half()
     assert torch.equal(gathered, ref)
     assert t == 1.5
+    # the self-verifying fields of the N > 1 bench line
+    assert dp["ranks_seen"] == 2 and dp["backend"] == "gloo"
+    assert dp["allgather_ms"] is not None and dp["allgather_ms"] >= 0
+    assert dp["allgather_bytes_per_rank"] == 3 * 3 * 64 * 64 * 2
+    assert dp["gather_slices_bitwise_equal"] is True and dp["gather_mismatched_ranks"] == 0
+    assert dp_bad["gather_slices_bitwise_equal"] is False and dp_bad["gather_mismatched_ranks"] == 1
 
 
 def _run_bench(args, env_extra=None):
@@ -151,6 +164,9 @@ def test_launch_ranks_spawns_ranks_and_gathers_rank_major(tmp_path):
     z, _ = _StubSampler().sample(4, 2 * 3, (4, 8, 8), conditioning=cg, x_T=xg)
     assert torch.equal(res["gathered"], _StubLD().decode_first_stage(z).half())
     assert res["elapsed"] > 0
+    dp = res["dp"]
+    assert dp["ranks_seen"] == 2 and dp["backend"] == "gloo" and dp["gather_slices_bitwise_equal"] is True
+    assert dp["allgather_ms"] is not None and res["n_timed_gathers"] == 2
 
 
 def test_launch_ranks_propagates_a_failing_rank(tmp_path):

@@ -75,12 +75,15 @@ def test_conv_plan_picks_skinny_and_names_every_variant(sdk):
     a.ho = s.h = 65                                    # 65 rows: a tiled plan
     assert L.sdk_conv2d_plan(C.byref(a), C.byref(info)) == 0, L.sdk_last_error()
     assert info.variant != 35
+    a.variant_hint = 6                                 # the retired variant 5 plans as 22 (the same 256x320 tile)
+    assert L.sdk_conv2d_plan(C.byref(a), C.byref(info)) == 0, L.sdk_last_error()
+    assert info.variant == 22
     a.variant_hint = 36
     assert L.sdk_conv2d_plan(C.byref(a), C.byref(info)) != 0         # forced 35 on 65 rows
     a.variant_hint = 37                                # the retired halo-tile ids 36 / 37 are unknown
     assert L.sdk_conv2d_plan(C.byref(a), C.byref(info)) != 0
     assert L.sdk_kernel_name(36) == b"unknown" and L.sdk_kernel_name(37) == b"unknown"
-    a.variant_hint = 39
+    a.variant_hint = 42
     assert L.sdk_conv2d_plan(C.byref(a), C.byref(info)) != 0         # unknown id
 
 

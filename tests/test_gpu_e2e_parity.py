@@ -13,7 +13,7 @@
   and a free-running 10-step v-prediction chain + decode vs the oracle's (a 50-step fp32 chain at 96²
   would take ~6 min of CPU).
 Every comparison prints and asserts rel-L2 AND max-abs error (relative to the oracle's max-abs); the
-thresholds are ~3x the errors measured on MI355X (profiles/r3_parity_errors.txt)."""
+thresholds are ~3x the errors measured on MI355X (profiles/r5_parity_errors.txt, r6_parity_errors.txt)."""
 import os
 import sys
 import time
@@ -123,9 +123,8 @@ def test_c3_bench_step_vs_oracle_chain(sdk):
     ref, _ = _oracle_chain(cfg, usd, vsd, xT[0:1].cpu(), ctx[0:1].cpu(), ld.scale_factor)
     print(f"[parity] C3 oracle chain: {time.time() - t0:.0f} s", flush=True)
     # free-running: the GPU's per-step error (~2e-3, teacher-forced above) integrated over 50 steps and
-    # magnified by the chain (amplification above): measured 2.36e-3 / 3.67e-3 (profiles/r3_parity_errors.txt;
-    # the 2.05e-2 / 8.5e-2 seen earlier in round 3 came from the fused-norm3 corruption,
-    # profiles/r3_xattn_determinism.txt) -> limits ~3.5x / 5x
+    # magnified by the chain (amplification above): measured 2.39e-3 / 3.17e-3 (profiles/r5_parity_errors.txt)
+    # -> limits ~3.3x / 3.2x
     _report("C3 image 0 free-running (50 DDIM steps + decode, B=16 bench step)", img[0:1], ref, 8e-3, 1e-2)   # 2.39e-3 / 3.17e-3
 
 
