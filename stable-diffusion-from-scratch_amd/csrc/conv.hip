@@ -1264,6 +1264,19 @@ __device__ __forceinline__ void item_coords(const Params& p, int it, int& tm, in
   sidx = slab - tn * p.split;
 }
 
+// sched_group_barrier sequence of the pipelined 16x16x32 K-step (conv_glds_kernel, PFD > 0): per MFMA group g the
+// W fragment read PFD groups ahead (DS read), the group's FM MFMAs, then its np DMA pieces (VMEM)
+template <int G, int PFD, int FM, int PPG, int GPW, int g = 0>
+__device__ __forceinline__ void pin_fragment_groups() {
+  if constexpr (g < G) {
+    if constexpr (g + PFD < G) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, FM, 0);
+    constexpr int np = GPW - g * PPG < 0 ? 0 : (GPW - g * PPG < PPG ? GPW - g * PPG : PPG);
+    if constexpr (np > 0) __builtin_amdgcn_sched_group_barrier(0x020, np, 0);
+    pin_fragment_groups<G, PFD, FM, PPG, GPW, g + 1>();
+  }
+}
+
 // One (tile, K-split) work item per workgroup, two LDS stages.
 // SIMPLE: the instantiation for one-segment, one-source convs without masks (build_params sets p.simple:
 // token GEMMs and the 3x3 convs over zero-bordered inputs): a lane's A row offset is fixed (the tap window's
@@ -1534,6 +1547,13 @@ __global__ void __launch_bounds__(CF::NT, CF::OCC * CF::NW / 4) conv_glds_kernel
             if (g * PPG + r < GPW) SDK_PIECE(q, g * PPG + r < GPW ? g * PPG + r : 0, wbuf);
         }
       }
+      if constexpr (PFD > 0 && SIMPLE != 0) {
+        // pin the order the fragment pipeline needs (the scheduler otherwise sinks each W read to just before its
+        // MFMAs next to a DMA issue, and the MFMAs wait lgkmcnt(0) on it): the up-front reads, then per group the
+        // read PFD groups ahead, the group's MFMAs and its DMA pieces
+        __builtin_amdgcn_sched_group_barrier(0x100, NKA * CF::FM16 + PFD, 0);
+        pin_fragment_groups<G, PFD, CF::FM16, (2 * GPW + G - 1) / G, GPW>();
+      }
     } else {
 #pragma unroll
       for (int kk = 0; kk < BK / 16; ++kk) {
@@ -1699,6 +1719,7 @@ __global__ void __launch_bounds__(CF::NT, CF::OCC * CF::NW / 4) conv_glds_kernel
         p, m0, n0, [&](int w) { return reinterpret_cast<const float2*>(lds + w * WSCR + scratch_halfs); });
   };
   if constexpr (CF::M16) {
+    static_assert(CF::FN16 % 4 == 0 || CF::FN16 % 4 == 2, "epilogue16_tile groups: 64- and 32-channel groups");
     if (lds_epi && p.gnp) {
       epilogue16_tile<CF::FM16, CF::FN16, true>(p, acc16, m0, n0, wm * CF::TM, wn * CF::TN, wscr, bias_s, rb_s);
       gn_store(EPG_BYTES / 2, std::integral_constant<int, 16>{});
@@ -2913,7 +2934,8 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
   // 16..19 deep-ring LDS-DMA configs; 20, 21 phased 256x256 on v_mfma_f32_16x16x32_f16;
   // 22..26 LDS-DMA configs 256x320, 7, 6, 19, 18 on v_mfma_f32_16x16x32_f16 (5 retired); 27..30 diagnostics;
   // 31, 32 two-per-CU 128x160 / 128x128 (16x16x32); 33 128x160 with a 4-stage ring; 34 direct (<= 8 outputs);
-  // 38 8-wave 256x320, 40 8-wave 256x256 (16x16x32; 39, the 256x320 on 32x32x16, spilled and is not built).
+  // 38 8-wave 256x320, 40 8-wave 256x256 (16x16x32, 64 / 128-row wave tiles; 39, the 256x320 on 32x32x16, spilled
+  // and is not built).
   // The diagnostic ablations compute wrong outputs by design: the product library rejects them,
   // only the separate diagnostics build (-DSDK_CONV_DIAGNOSTICS, libsdk_amd_diag.so) runs them.
   if (is_diagnostic_variant(forced) && !kDiagnostics)

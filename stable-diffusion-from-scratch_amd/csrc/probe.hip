@@ -15,8 +15,11 @@ namespace sdk {
 typedef unsigned int u4 __attribute__((ext_vector_type(4)));
 namespace {
 
+// (__launch_bounds__(256, 2): with the default bounds hipcc kept the 16x16x32 accumulators in AGPRs and copied all
+// 32 of them through VGPRs every iteration — 48 accvgpr moves per 8 MFMAs — and the probe read 1.19 PF/s; with the
+// occupancy stated the loop is 8 bare MFMAs, as the conv kernels' are)
 template <bool M16>
-__global__ void __launch_bounds__(256) mfma_probe_kernel(const half_t* seed, int iters, float* sink) {
+__global__ void __launch_bounds__(256, 2) mfma_probe_kernel(const half_t* seed, int iters, float* sink) {
   const int lane = threadIdx.x & 63;
   h8 a = *reinterpret_cast<const h8*>(seed + (size_t)((blockIdx.x * 256 + threadIdx.x) & 4095) * 8);
   h8 b = *reinterpret_cast<const h8*>(seed + (size_t)((blockIdx.x * 256 + threadIdx.x + 1777) & 4095) * 8);

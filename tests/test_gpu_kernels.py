@@ -43,7 +43,7 @@ def _conv_ref(x_nhwc, w, b, stride=1, pad=1, upsample=False, gn=None, silu=False
 
 
 @pytest.fixture(params=["auto", "0", "2", "3", "4", "6", "7", "8", "9", "16", "17", "18", "19", "20", "21",
-                        "22", "23", "24", "25", "26", "31", "32", "33"])
+                        "22", "23", "24", "25", "26", "31", "32", "33", "38", "40"])
 def conv_variant(request, sdk):
     """Every conv kernel variant (register-staged 128x128, LDS-DMA 256x256/256x128/128x128)."""
     from sd_amd import ops as o
@@ -336,7 +336,7 @@ def test_group_norm_apply_concat(ops, silu):
     assert rel_l2(y, ref.permute(0, 2, 3, 1)) < 1e-3
 
 
-GLDS_VARIANTS = {2, 3, 4, 6, 7, 16, 17, 18, 19, 22, 23, 24, 25, 26, 31, 32, 33}
+GLDS_VARIANTS = {2, 3, 4, 6, 7, 16, 17, 18, 19, 22, 23, 24, 25, 26, 31, 32, 33, 38, 40}
 
 
 def _chunk_stats(y, nch):
@@ -656,3 +656,4 @@ def test_upsample_nearest2x_padded(ops, B, H, W, C, ldx):
             a = ops.conv2d(pc, x.contiguous(), upsample=True, pad=1, variant=v, split_k=1)
             b = ops.conv2d(pc, y, pad=0, variant=v, split_k=1)
             assert torch.equal(a, b), f"variant {v}"
+
