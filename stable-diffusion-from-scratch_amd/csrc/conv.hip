@@ -81,16 +81,24 @@ struct Params {
   unsigned* tcnt;
   int gm;               // unsplit plans: tiles visited in groups of gm M-panels, N-tile major inside a group
   unsigned long long* stamps;   // diagnostics build only: 8 shader-clock stamps per workgroup, or null
+  int stamps_rt;                // diagnostics: slots 6 / 7 = s_memrealtime at entry / end (SDK_CONV_STAMPS=2)
   int simple;           // token GEMM (one segment, 1x1 stride 1, no masks, one source): linear A / W K offsets
 };
 
 // diagnostics build: s_memtime at kernel entry / after the prologue / after the K loop / at the end (+ after
 // epilogue groups 0-3 at 4-7), by
 // thread 0 of every workgroup (sdk_diag_conv_stamps copies them out); compiled out of the product library
+// SDK_CONV_STAMPS=2: slots 6 / 7 hold s_memrealtime (100 MHz) at entry / end instead of epilogue groups 2 / 3, so the
+// shader clock the workgroup ran at is (memtime end - entry) / (realtime end - entry) x 100 MHz (MI355X_MICROARCH.md
+// 'DVFS give-back' item 6)
 __device__ __forceinline__ void ph_stamp(const Params& p, int i) {
 #ifdef SDK_CONV_DIAGNOSTICS
-  if (p.stamps && threadIdx.x == 0)
-    p.stamps[((size_t)blockIdx.x + (size_t)blockIdx.y * gridDim.x) * 8 + i] = __builtin_amdgcn_s_memtime();
+  if (p.stamps && threadIdx.x == 0) {
+    const size_t wg = ((size_t)blockIdx.x + (size_t)blockIdx.y * gridDim.x) * 8;
+    if (p.stamps_rt && i >= 6) return;
+    p.stamps[wg + i] = __builtin_amdgcn_s_memtime();
+    if (p.stamps_rt && (i == 0 || i == 3)) p.stamps[wg + (i == 0 ? 6 : 7)] = __builtin_amdgcn_s_memrealtime();
+  }
 #endif
 }
 
@@ -2998,6 +3006,7 @@ int build_params(const sdk_conv_args* a, Params& p, sdk_conv_plan_info* info) {
     if (!g_conv_stamps && (hipMalloc((void**)&g_conv_stamps, (size_t)kStampWgs * 8 * 8) != hipSuccess ||
                            hipMemset(g_conv_stamps, 0, (size_t)kStampWgs * 8 * 8) != hipSuccess)) g_conv_stamps = nullptr;
     if ((long long)p.tiles_m * p.tiles_n * p.split <= kStampWgs) p.stamps = g_conv_stamps;
+    p.stamps_rt = atoi(getenv("SDK_CONV_STAMPS")) == 2;
   }
 #endif
   int64_t ws = split > 1 ? (int64_t)split * p.M * p.Npad * 4 : 0;

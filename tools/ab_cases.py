@@ -43,6 +43,19 @@ def main():
     from sd_amd import ops
     cases = sys.argv[1:] or DEFAULT
     reps = int(os.environ.get("AB_REPS", "5"))
+    # the clock under sustained load (MI355X_MICROARCH.md 'DVFS give-back'): short bursts after idle run below it —
+    # round 6 measured the 64x64 3x3 conv at 110-118 us in bursts and 95 us after 2 s of back-to-back launches
+    # (tools/conv_stamps.py, profiles/r6_conv_ablation.txt) — so a busy loop of AB_WARM_S seconds comes first
+    warm_s = float(os.environ.get("AB_WARM_S", "2"))
+    if warm_s > 0:
+        import time
+        a = torch.randn(8192, 8192, device="cuda", dtype=torch.float16)
+        t0 = time.time()
+        while time.time() - t0 < warm_s:
+            for _ in range(8):
+                a @ a
+            torch.cuda.synchronize()
+        del a
     for c in cases:
         name, spec = c.split(":")
         v = [int(t) for t in spec.split(",")]

@@ -21,9 +21,23 @@ def main():
     pc = ops.PackedConv([(w, Ci)], torch.zeros(Co, device="cuda"), geglu=bool(geglu), device="cuda")
     kw = dict(stride=st, pad=k // 2 if "prepad" not in name else 0, upsample=bool(up), variant=variant, split_k=1,
               out_mode=ops.OUT_GEGLU_F16 if geglu else ops.OUT_NHWC_F16)
-    for _ in range(3):
+    import time
+    warm = float(os.environ.get("STAMP_WARM_S", "0"))   # back-to-back launches first: the clock under sustained load
+    t0 = time.time()
+    while True:
+        for _ in range(3):
+            ops.conv2d(pc, x, **kw)
+        torch.cuda.synchronize()
+        if time.time() - t0 >= warm:
+            break
+    # launch time in this same process and clock state: 20 back-to-back launches between HIP events
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(20):
         ops.conv2d(pc, x, **kw)
-    torch.cuda.synchronize()
+    e1.record()
+    e1.synchronize()
+    print(f"{name} v{variant}: {e0.elapsed_time(e1) / 20 * 1e3:.1f} us per launch (20 back-to-back, HIP events)")
     ops.conv2d(pc, x, **kw)
     torch.cuda.synchronize()
     info = ops.ConvPlanInfo()
@@ -43,6 +57,16 @@ def main():
     ep = (live[:, 3] - live[:, 2]).mean()
     print(f"{name} v{variant}: {len(live)} workgroups; mean cycles prologue {pro:.0f}  K loop {kl:.0f}  "
           f"epilogue {ep:.0f}  lifetime {(live[:, 3] - live[:, 0]).mean():.0f}")
+    if os.environ.get("SDK_CONV_STAMPS") == "2":   # slots 6 / 7: s_memrealtime (100 MHz) at entry / end
+        rt = live[(live[:, 7] > live[:, 6])]
+        clk = (rt[:, 3] - rt[:, 0]) / ((rt[:, 7] - rt[:, 6]) / 100e6) / 1e9
+        print(f"   shader clock over the workgroup lifetimes: median {np.median(clk):.3f} GHz "
+              f"[{clk.min():.3f}-{clk.max():.3f}]; lifetime {np.median((rt[:, 7] - rt[:, 6]) / 100.0):.1f} us (realtime)")
+        st, en = (rt[:, 6] - rt[:, 6].min()) / 100.0, (rt[:, 7] - rt[:, 6].min()) / 100.0
+        print(f"   realtime span first start -> last end {en.max():.1f} us; starts spread {np.percentile(st, 50):.1f} / "
+              f"{np.percentile(st, 90):.1f} / {st.max():.1f} us (p50 / p90 / max), ends {np.percentile(en, 10):.1f} / "
+              f"{np.percentile(en, 50):.1f} / {en.max():.1f} us (p10 / p50 / max)")
+        return
     g = live[live[:, 4] > 0]
     if len(g):
         prev = g[:, 2]
