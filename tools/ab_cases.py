@@ -1,6 +1,6 @@
 """Time conv / GEMM cases on the device (graph-replayed launches, median of reps, random data) — the
 per-kernel A/B driver: run once per library (SD_AMD_LIB selects an A/B build) and compare the lines.
-usage: python tools/ab_cases.py [case ...]; case = name:B,H,W,Ci,Co,k,pad,variant,split[,geglu[,residual]]
+usage: python tools/ab_cases.py [case ...]; case = name:B,H,W,Ci,Co,k,pad,variant,split[,geglu[,residual[,gn_stats[,emb]]]]
 (no cases: the default SD-1 list below).  Prints '<name> v<variant> s<split> <us> us <TF/s>'."""
 import os
 import sys
@@ -62,12 +62,18 @@ def main():
         B, H, W, Ci, Co, k, pad, variant, split = v[:9]
         geglu = len(v) > 9 and v[9] == 1
         with_res = len(v) > 10 and v[10] == 1
+        with_gn = len(v) > 11 and v[11] == 1      # the epilogue emits GroupNorm statistics (ResBlock convs)
+        with_emb = len(v) > 12 and v[12] == 1     # per-(image, channel) embedding row (ResBlock conv1)
         torch.manual_seed(0)
         x = torch.randn(B, H, W, Ci, device="cuda").half()
         w = torch.randn(Co, Ci, k, k, device="cuda") / (Ci * k * k) ** 0.5
         pc = ops.PackedConv([(w, Ci)], torch.randn(Co, device="cuda") * 0.1, geglu=geglu, device="cuda")
         mode = ops.OUT_GEGLU_F16 if geglu else ops.OUT_NHWC_F16
         kw = dict(pad=pad, variant=variant, split_k=split, out_mode=mode)
+        if with_gn:
+            kw["gn_stats"] = True
+        if with_emb:
+            kw["row_bias"] = (torch.randn(B, Co, device="cuda"), 0)
         if with_res:
             Ho, Wo = (H + 2 * pad - k) + 1, (W + 2 * pad - k) + 1
             kw["residual"] = torch.randn(B, Ho, Wo, Co, device="cuda").half()
