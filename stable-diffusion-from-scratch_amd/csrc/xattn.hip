@@ -46,6 +46,7 @@ __device__ __forceinline__ void stamp(const XAttnParams& p, int i) {
 }
 
 unsigned long long* g_xattn_stamps = nullptr;
+int g_xattn_waves640 = 8;
 
 typedef _Float16 h4v __attribute__((ext_vector_type(4)));
 typedef __fp16 fp16x4_t __attribute__((ext_vector_type(4)));
@@ -53,14 +54,18 @@ typedef __fp16 fp16x4_t __attribute__((ext_vector_type(4)));
 constexpr int XQ = 64;     // query rows per workgroup
 constexpr int XKP = 80;    // key slots (5 blocks of 16)
 
-template <int C, int D>
+// NWV waves: 4 (one channel quarter of the projections each) or, at 640 channels, 8 (one channel eighth
+// each: the wave's projection tile is then the 320-channel kernel's 80 channels x 64 rows, whose
+// registers allow 2 waves per SIMD where the 4-wave 640 form holds 512 registers per lane and runs one
+// wave per SIMD; in the head phase the two waves of a row group take one head each)
+template <int C, int D, int NWV = 4>
 struct XCfg {
-  static constexpr int NT = 256;                    // 4 waves, one channel quarter each
+  static constexpr int NT = 64 * NWV;
   static constexpr int H = C / D;
   static constexpr int DP = (D + 15) / 16 * 16;     // head dim padded to the 16-wide MFMA K / N
-  static constexpr int CW = C / 4;                  // channels per wave in the projections
+  static constexpr int CW = C / NWV;                // channels per wave in the projections
   static constexpr int NB = CW / 16;
-  static constexpr int WP = C <= 320 ? 3 : 4;      // W prefetch depth (K-steps): 320 keeps 2 waves / SIMD
+  static constexpr int WP = C <= 320 || NWV == 8 ? 3 : 4;   // W prefetch depth (K-steps): keeps 2 waves / SIMD
   static constexpr int QLD = C + 8;                 // q / o row stride (halfs); 8 zero pad columns
   static constexpr int KLD = DP + 8;                // K rows [key][d]
   // V rows [key][d] (row-major, 16-B copies like K; the PV operand V^T is read with ds_read_b64_tr_b16):
@@ -75,6 +80,8 @@ struct XCfg {
   static constexpr int LDS_HALFS = XQ * QLD + HPI * KVH;
   static constexpr int LDS_BYTES = LDS_HALFS * 2;
   static_assert(C % 64 == 0 && CW % 16 == 0 && D % 8 == 0 && C % D == 0, "shape");
+  static_assert(NWV == 4 || (NWV == 8 && HPI == 2), "8 waves: one head per wave of a row group pair");
+  static constexpr int GPW = NWV == 8 ? 1 : HPI;    // heads per wave and iteration
   static_assert(DP - D <= 8, "q padding columns cover the last head's d padding");
   static_assert(LDS_BYTES <= 160 * 1024, "LDS");
 };
@@ -150,29 +157,30 @@ __device__ __forceinline__ void ln_quad_rows(const half_t* src, int ld, const fl
 // gamma | beta (fp32, C each) of a fused norm: GBT 16-B pieces per thread, loaded into registers
 // well ahead of use (under the kernel's own HBM stream an L2 miss costs microseconds), then
 // written to the LDS staging area
-template <int C>
+template <int C, int NT>
 struct LnStage {
-  static constexpr int GBT = (C / 2 + 255) / 256;
+  static constexpr int GBT = (C / 2 + NT - 1) / NT;
   f4 r[GBT];
   __device__ __forceinline__ void load(const float* gamma, const float* beta) {
 #pragma unroll
     for (int u = 0; u < GBT; ++u) {
-      const int e = threadIdx.x + 256 * u;
+      const int e = threadIdx.x + NT * u;
       if (e < C / 2) r[u] = *reinterpret_cast<const f4*>(e < C / 4 ? gamma + 4 * e : beta + 4 * (e - C / 4));
     }
   }
   __device__ __forceinline__ void store(float* gb) const {
 #pragma unroll
     for (int u = 0; u < GBT; ++u) {
-      const int e = threadIdx.x + 256 * u;
+      const int e = threadIdx.x + NT * u;
       if (e < C / 2) *reinterpret_cast<f4*>(gb + 4 * e) = r[u];
     }
   }
 };
 
-template <int C, int D>
-__global__ void __launch_bounds__(256, 1) xattn_block_kernel(XAttnParams p) {
-  using X = XCfg<C, D>;
+template <int C, int D, int NWV>
+__global__ void __launch_bounds__(64 * NWV, 1) xattn_block_kernel(XAttnParams p) {
+  using X = XCfg<C, D, NWV>;
+  constexpr int NT = X::NT;
   extern __shared__ __attribute__((aligned(16))) half_t xl[];
   half_t* qo = xl;                              // [64][QLD]
   half_t* kvl = qo + XQ * X::QLD;               // HPI x { K [80][KLD], V [80][VLD] }
@@ -184,41 +192,42 @@ __global__ void __launch_bounds__(256, 1) xattn_block_kernel(XAttnParams p) {
 
   static_assert(2 * C * 4 <= X::HPI * X::KVH * 2, "norm gamma / beta staging fits the K / V^T area");
   float* gbl = reinterpret_cast<float*>(kvl);
-  LnStage<C> ln2;
+  LnStage<C, NT> ln2;
   if (p.ln_in_g) ln2.load(p.ln_in_g, p.ln_in_b);
   // zero the q pad columns (the K / V^T padding is zeroed after norm2 has used that area)
-  for (int e = tid; e < XQ * 8; e += 256) qo[(e >> 3) * X::QLD + C + (e & 7)] = (half_t)0.f;
+  for (int e = tid; e < XQ * 8; e += NT) qo[(e >> 3) * X::QLD + C + (e & 7)] = (half_t)0.f;
   stamp(p, 0);
   // ---- phase A: q = t Wq^T -> LDS (fp16, as the separate to_q GEMM stores it).  The t tile is
   // staged into the q buffer first with every 16-B load in flight at once (one HBM latency
   // instead of one per K-step); q overwrites it after all waves are past their MFMAs.
   {
     constexpr int C8 = C / 8;
-    constexpr int TL = XQ * C8 / 256;           // 16-B chunks per thread
-    static_assert(XQ * C8 % 256 == 0, "t tile chunks");
+    constexpr int TL = XQ * C8 / NT;            // 16-B chunks per thread
+    static_assert(XQ * C8 % NT == 0, "t tile chunks");
     h8 tv[TL];
 #pragma unroll
     for (int u = 0; u < TL; ++u) {
-      const int e = tid + 256 * u, row = e / C8, c8 = e - row * C8;
+      const int e = tid + NT * u, row = e / C8, c8 = e - row * C8;
       tv[u] = *reinterpret_cast<const h8*>(p.t + (size_t)(m0 + row) * p.t_ld + 8 * c8);
     }
 #pragma unroll
     for (int u = 0; u < TL; ++u) {
-      const int e = tid + 256 * u, row = e / C8, c8 = e - row * C8;
+      const int e = tid + NT * u, row = e / C8, c8 = e - row * C8;
       *reinterpret_cast<h8*>(qo + row * X::QLD + 8 * c8) = tv[u];
     }
     if (p.ln_in_g) ln2.store(gbl);
   }
   __syncthreads();
-  if (p.ln_in_g) {   // norm2 in place: t = LN(tokens)
-    ln_quad_rows<C>(qo, X::QLD, gbl, p.ln_in_eps,
+  if (p.ln_in_g) {   // norm2 in place: t = LN(tokens); rows 16w .. 16w + 15 on waves 0-3
+    if (wave < 4)
+      ln_quad_rows<C>(qo, X::QLD, gbl, p.ln_in_eps,
                     [&](int row, int c, const h8& v) { *reinterpret_cast<h8*>(qo + row * X::QLD + c) = v; });
     __syncthreads();
   }
   // K / V^T padding (keys >= nk, d >= D) stays zero through phase B; phase A's barriers order this
   // before the first K / V^T writes
   static_assert(X::HPI * X::KVH % 8 == 0, "K / V^T area in 16-B pieces");
-  for (int e = tid; e < X::HPI * X::KVH / 8; e += 256) reinterpret_cast<h8*>(kvl)[e] = h8{};
+  for (int e = tid; e < X::HPI * X::KVH / 8; e += NT) reinterpret_cast<h8*>(kvl)[e] = h8{};
   stamp(p, 1);
   {
     f4 acc[X::NB][4];
@@ -242,10 +251,11 @@ __global__ void __launch_bounds__(256, 1) xattn_block_kernel(XAttnParams p) {
   // iterations' heads are loaded into registers KVA iterations ahead and written to LDS after
   // the current iteration's closing barrier.
   const half_t* kvb = p.kv + (size_t)b * p.nk * p.kv_ld;
-  const int qrow = 16 * wave + r16;             // this lane's query (S^T column)
-  constexpr int HPI = X::HPI;
+  const int qrow = 16 * (wave & 3) + r16;       // this lane's query (S^T column)
+  constexpr int HPI = X::HPI, GPW = X::GPW;
+  const int g0 = NWV == 8 ? wave >> 2 : 0;      // the wave's first head slot of an iteration
   constexpr int CH = D / 8;                     // 16-B chunks per key row
-  constexpr int NCH = (XKP * CH + 255) / 256;   // chunks per thread per head
+  constexpr int NCH = (XKP * CH + NT - 1) / NT; // chunks per thread per head
   constexpr int NIT = (X::H + HPI - 1) / HPI;
   constexpr int KVA = HPI == 2 ? 1 : 2;          // iterations of K / V prefetch (register budget)
   h8 rk[KVA][HPI][NCH], rv[KVA][HPI][NCH];
@@ -255,7 +265,7 @@ __global__ void __launch_bounds__(256, 1) xattn_block_kernel(XAttnParams p) {
       const int h = it * HPI + g;
 #pragma unroll
       for (int u = 0; u < NCH; ++u) {
-        const int e = tid + 256 * u;
+        const int e = tid + NT * u;
         const int key = e / CH, ch = e - key * CH;
         if (key < p.nk && h < X::H) {
           const half_t* src = kvb + (size_t)key * p.kv_ld + h * D + 8 * ch;
@@ -276,7 +286,7 @@ __global__ void __launch_bounds__(256, 1) xattn_block_kernel(XAttnParams p) {
       half_t* vr = kl + XKP * X::KLD;
 #pragma unroll
       for (int u = 0; u < NCH; ++u) {
-        const int e = tid + 256 * u;
+        const int e = tid + NT * u;
         const int key = e / CH, ch = e - key * CH;
         if (key < p.nk && it * HPI + g < X::H) {
           *reinterpret_cast<h8*>(kl + key * X::KLD + 8 * ch) = rk[sl][g][u];
@@ -289,13 +299,14 @@ __global__ void __launch_bounds__(256, 1) xattn_block_kernel(XAttnParams p) {
     __builtin_amdgcn_sched_barrier(0);
     const int ng = X::H - it * HPI < HPI ? X::H - it * HPI : HPI;   // heads this iteration
     // S^T[key, q] for the 5 key blocks of each head
-    f4 s[HPI][XKP / 16];
+    f4 s[GPW][XKP / 16];
 #pragma unroll
-    for (int g = 0; g < HPI; ++g)
+    for (int gi = 0; gi < GPW; ++gi)
 #pragma unroll
-      for (int kb = 0; kb < XKP / 16; ++kb) s[g][kb] = f4{};
+      for (int kb = 0; kb < XKP / 16; ++kb) s[gi][kb] = f4{};
 #pragma unroll
-    for (int g = 0; g < HPI; ++g) {
+    for (int gi = 0; gi < GPW; ++gi) {
+      const int g = g0 + gi;
       if (g < ng) {
         const int h = it * HPI + g;
         const half_t* kl = kvl + g * X::KVH;
@@ -305,16 +316,16 @@ __global__ void __launch_bounds__(256, 1) xattn_block_kernel(XAttnParams p) {
 #pragma unroll
           for (int kb = 0; kb < XKP / 16; ++kb) {
             const h4v fk = *reinterpret_cast<const h4v*>(kl + (16 * kb + r16) * X::KLD + dd + 4 * c16);
-            s[g][kb] = __builtin_amdgcn_mfma_f32_16x16x16f16(fk, fq, s[g][kb], 0, 0, 0);
+            s[gi][kb] = __builtin_amdgcn_mfma_f32_16x16x16f16(fk, fq, s[gi][kb], 0, 0, 0);
           }
         }
       }
     }
     // lane holds keys 16kb + 4*c16 + r of query qrow
-    float mx[HPI], sum[HPI], inv[HPI];
-    h4v pf[HPI][XKP / 16];
+    float mx[GPW], sum[GPW], inv[GPW];
+    h4v pf[GPW][XKP / 16];
 #pragma unroll
-    for (int g = 0; g < HPI; ++g) {
+    for (int g = 0; g < GPW; ++g) {
       mx[g] = -__builtin_inff();
 #pragma unroll
       for (int kb = 0; kb < XKP / 16; ++kb)
@@ -327,11 +338,11 @@ __global__ void __launch_bounds__(256, 1) xattn_block_kernel(XAttnParams p) {
         }
     }
 #pragma unroll
-    for (int g = 0; g < HPI; ++g) mx[g] = fmaxf(mx[g], __shfl_xor(mx[g], 16, 64));
+    for (int g = 0; g < GPW; ++g) mx[g] = fmaxf(mx[g], __shfl_xor(mx[g], 16, 64));
 #pragma unroll
-    for (int g = 0; g < HPI; ++g) mx[g] = fmaxf(mx[g], __shfl_xor(mx[g], 32, 64));
+    for (int g = 0; g < GPW; ++g) mx[g] = fmaxf(mx[g], __shfl_xor(mx[g], 32, 64));
 #pragma unroll
-    for (int g = 0; g < HPI; ++g) {
+    for (int g = 0; g < GPW; ++g) {
       sum[g] = 0.f;
 #pragma unroll
       for (int kb = 0; kb < XKP / 16; ++kb)
@@ -343,9 +354,9 @@ __global__ void __launch_bounds__(256, 1) xattn_block_kernel(XAttnParams p) {
         }
     }
 #pragma unroll
-    for (int g = 0; g < HPI; ++g) sum[g] += __shfl_xor(sum[g], 16, 64);
+    for (int g = 0; g < GPW; ++g) sum[g] += __shfl_xor(sum[g], 16, 64);
 #pragma unroll
-    for (int g = 0; g < HPI; ++g) {
+    for (int g = 0; g < GPW; ++g) {
       sum[g] += __shfl_xor(sum[g], 32, 64);
       inv[g] = 1.f / sum[g];
     }
@@ -355,7 +366,8 @@ __global__ void __launch_bounds__(256, 1) xattn_block_kernel(XAttnParams p) {
     // (EXEC is all ones here: g < ng is wave-uniform)
     const int tr_off = (4 * c16 + ((lane & 15) >> 2)) * X::VLD + 4 * (lane & 3);
 #pragma unroll
-    for (int g = 0; g < HPI; ++g) {
+    for (int gi = 0; gi < GPW; ++gi) {
+      const int g = g0 + gi;
       if (g < ng) {
         const int h = it * HPI + g;
         const half_t* vr = kvl + g * X::KVH + XKP * X::KLD;
@@ -367,13 +379,13 @@ __global__ void __launch_bounds__(256, 1) xattn_block_kernel(XAttnParams p) {
             const auto t4 = __builtin_amdgcn_ds_read_tr16_b64_v4f16(
                 (__attribute__((address_space(3))) fp16x4_t*)(vr + 16 * kb * X::VLD + dd + tr_off));
             const h4v fv = __builtin_bit_cast(h4v, t4);
-            o = __builtin_amdgcn_mfma_f32_16x16x16f16(fv, pf[g][kb], o, 0, 0, 0);
+            o = __builtin_amdgcn_mfma_f32_16x16x16f16(fv, pf[gi][kb], o, 0, 0, 0);
           }
           const int d0 = dd + 4 * c16;          // lane holds d0..d0+3 of query qrow
           if (d0 < D) {
             h4v w;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) w[r] = (half_t)(o[r] * inv[g]);
+            for (int r = 0; r < 4; ++r) w[r] = (half_t)(o[r] * inv[gi]);
             *reinterpret_cast<h4v*>(qo + qrow * X::QLD + h * D + d0) = w;
           }
         }
@@ -385,7 +397,7 @@ __global__ void __launch_bounds__(256, 1) xattn_block_kernel(XAttnParams p) {
   stamp(p, 3);
   // ---- phase C: out = o Wo^T + bo (fp16) + residual, staged through LDS for row stores
   {
-    LnStage<C> ln3;
+    LnStage<C, NT> ln3;
     if (p.out_ln) ln3.load(p.ln_out_g, p.ln_out_b);
     f4 acc[X::NB][4];
     proj_wave<C, X::NB, X::WP>(qo, X::QLD, p.wo, n_w, acc);
@@ -408,7 +420,7 @@ __global__ void __launch_bounds__(256, 1) xattn_block_kernel(XAttnParams p) {
     if (p.out_ln) ln3.store(gbl);   // phase B is over: the K / V^T area is free
     __syncthreads();
     constexpr int C8 = C / 8;
-    for (int e = tid; e < XQ * C8; e += 256) {
+    for (int e = tid; e < XQ * C8; e += NT) {
       const int row = e / C8, c8 = e - row * C8;
       h8 v = *reinterpret_cast<const h8*>(qo + row * X::QLD + 8 * c8);
       const size_t m = (size_t)m0 + row;
@@ -424,20 +436,21 @@ __global__ void __launch_bounds__(256, 1) xattn_block_kernel(XAttnParams p) {
       __syncthreads();
       half_t* dst = p.out_ln + (size_t)m0 * p.out_ln_ld;
       const int ld = p.out_ln_ld;
-      ln_quad_rows<C>(qo, X::QLD, gbl, p.ln_out_eps,
+      if (wave < 4)
+        ln_quad_rows<C>(qo, X::QLD, gbl, p.ln_out_eps,
                       [&](int row, int c, const h8& v) { *reinterpret_cast<h8*>(dst + (size_t)row * ld + c) = v; });
     }
   }
   stamp(p, 5);
 }
 
-template <int C, int D>
+template <int C, int D, int NWV = 4>
 int launch_xattn(const XAttnParams& p, int m, hipStream_t s) {
-  using X = XCfg<C, D>;
+  using X = XCfg<C, D, NWV>;
   static std::atomic<unsigned long long> attr{0};
-  if (int e = ensure_dyn_lds((const void*)xattn_block_kernel<C, D>, X::LDS_BYTES, attr, "cross_attention_block"))
+  if (int e = ensure_dyn_lds((const void*)xattn_block_kernel<C, D, NWV>, X::LDS_BYTES, attr, "cross_attention_block"))
     return e;
-  hipLaunchKernelGGL((xattn_block_kernel<C, D>), dim3(m / XQ), dim3(X::NT), X::LDS_BYTES, s, p);
+  hipLaunchKernelGGL((xattn_block_kernel<C, D, NWV>), dim3(m / XQ), dim3(X::NT), X::LDS_BYTES, s, p);
   return check_launch("xattn_block");
 }
 
@@ -484,6 +497,12 @@ using namespace sdk;
 // diagnostics only (not in sdk_amd.h): per-workgroup phase clock stamps into a device buffer of
 // 8 * groups uint64 (wall_clock64, 100 MHz), for tools/bench_xattn.py --phases; null turns it off
 extern "C" void sdk_xattn_debug_stamps(unsigned long long* dev) { g_xattn_stamps = dev; }
+// A/B only (not in sdk_amd.h): waves of the 640-channel form, 8 (default) or 4
+extern "C" int sdk_xattn_debug_waves640(int waves) {
+  if (waves != 4 && waves != 8) return fail(SDK_EINVAL, "xattn waves: 4 or 8");
+  g_xattn_waves640 = waves;
+  return SDK_OK;
+}
 
 extern "C" int sdk_cross_attention_block_supported(int32_t channels, int32_t head_dim, int32_t nk, int32_t n_img) {
   const bool cd = (channels == 320 && (head_dim == 40 || head_dim == 64)) ||
@@ -525,7 +544,9 @@ int xattn_run(const sdk_xattn_args* a, const sdk_xattn_ln_args* ln, sdk_stream_t
   const int m = a->batch * a->n_img;
   hipStream_t s = (hipStream_t)stream;
   if (a->channels == 320) return a->head_dim == 40 ? launch_xattn<320, 40>(p, m, s) : launch_xattn<320, 64>(p, m, s);
-  return a->head_dim == 80 ? launch_xattn<640, 80>(p, m, s) : launch_xattn<640, 64>(p, m, s);
+  if (g_xattn_waves640 == 4)
+    return a->head_dim == 80 ? launch_xattn<640, 80, 4>(p, m, s) : launch_xattn<640, 64, 4>(p, m, s);
+  return a->head_dim == 80 ? launch_xattn<640, 80, 8>(p, m, s) : launch_xattn<640, 64, 8>(p, m, s);
 }
 }  // namespace
 

@@ -513,6 +513,35 @@ def test_cross_attention_block_fused_norms(ops, B, N, C, D, nk):
     assert torch.equal(y_out, y_sep) and torch.equal(t3_out, t3_sep)
 
 
+@pytest.mark.parametrize("B,N,D,nk", [(2, 1024, 80, 77), (2, 64, 64, 80), (1, 192, 80, 13)])
+def test_cross_attention_block_640_waves_bitwise(ops, B, N, D, nk):
+    """The 640-channel block's 8-wave form (the default: two waves per SIMD) and its 4-wave form (one wave
+    per SIMD) give the same bits, with and without the folded norms: per output element the K order of
+    both projections and the head math are the same, only the channels per wave differ."""
+    from sd_amd._lib import lib
+    C = 640
+    g = torch.Generator(device="cpu").manual_seed(11 * N + D + nk)
+    tok = (torch.randn(B * N, C, generator=g) * 2 + 0.5).half().to(DEV)
+    kv = torch.randn(B * nk, 2 * C, generator=g).half().to(DEV)
+    pcq = ops.PackedConv([(torch.randn(C, C, generator=g) / math.sqrt(C), C)], None, device=DEV)
+    pco = ops.PackedConv([(torch.randn(C, C, generator=g) / math.sqrt(C), C)], torch.randn(C, generator=g) * 0.1,
+                         device=DEV)
+    gg, bb = (1 + 0.1 * torch.randn(C, generator=g)).to(DEV), (0.1 * torch.randn(C, generator=g)).to(DEV)
+    kw = dict(batch=B, n_img=N, nk=nk, heads=C // D, head_dim=D, scale=D ** -0.5, residual=tok)
+    outs = {}
+    try:
+        for waves in (4, 8):
+            assert lib().sdk_xattn_debug_waves640(waves) == 0
+            y = ops.cross_attention_block(tok, kv, pcq, pco, **kw)
+            yn, t3 = ops.cross_attention_block(tok, kv, pcq, pco, norm_in=(gg, bb, 1e-5), norm_out=(gg, bb, 1e-5), **kw)
+            torch.cuda.synchronize()
+            outs[waves] = (y, yn, t3)
+    finally:
+        lib().sdk_xattn_debug_waves640(8)
+    for a, b in zip(outs[4], outs[8]):
+        assert torch.equal(a, b)
+
+
 def test_cross_attention_block_fused_norms_rejects(ops):
     C, D, N, nk = 320, 40, 64, 77
     t = torch.zeros(N, C, dtype=torch.float16, device=DEV)

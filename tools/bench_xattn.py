@@ -156,8 +156,56 @@ def reassoc():
               f"block's update {err:.2e}", flush=True)
 
 
+def ab_arms(which):
+    """The block with the norms folded (the UNet's form), A/B of two kernel settings in one process:
+    ``waves640`` = 4 vs 8 waves per workgroup at 640 channels (sdk_xattn_debug_waves640; bitwise equal).
+    5 alternating rounds of 20 launches each, median [min-max] per arm, bitwise check and rel-L2 of the
+    block update."""
+    import sd_amd_loader
+    sd_amd_loader.load()
+    from sd_amd import ops
+    from sd_amd._lib import lib
+    nk = 77
+    assert which == "waves640"
+    arms, setter, reset = (4, 8), lib().sdk_xattn_debug_waves640, 8
+    for name, B, N, C, D in SHAPES:
+        if (which == "waves640" and C != 640) or not ops.cross_attention_block_supported(C, D, nk, N):
+            continue
+        H = C // D
+        tok = torch.randn(B * N, C, device="cuda").half()
+        kv = torch.randn(B * nk, 2 * C, device="cuda").half()
+        pcq = ops.PackedConv([(torch.randn(C, C) / math.sqrt(C), C)], None, device="cuda")
+        pco = ops.PackedConv([(torch.randn(C, C) / math.sqrt(C), C)], torch.zeros(C), device="cuda")
+        g, b = torch.ones(C, device="cuda"), torch.zeros(C, device="cuda")
+        t3 = torch.empty_like(tok)
+        f = lambda: ops.cross_attention_block(tok, kv, pcq, pco, batch=B, n_img=N, nk=nk, heads=H, head_dim=D,
+                                              scale=D ** -0.5, residual=tok, norm_in=(g, b, 1e-5),
+                                              norm_out=(g, b, 1e-5), out_ln=t3)
+        res, outs = {a: [] for a in arms}, {}
+        for r in range(5):
+            for a in arms:
+                setter(a)
+                res[a].append(timeit(f))
+                if r == 0:
+                    y, _ = f()
+                    torch.cuda.synchronize()
+                    outs[a] = (y.clone(), t3.clone())
+        setter(reset)
+        same = all(torch.equal(x, y) for x, y in zip(outs[arms[0]], outs[arms[1]]))
+        y0, y1 = outs[arms[0]][0].float(), outs[arms[1]][0].float()
+        rel = ((y1 - y0).norm() / (y0 - tok.float()).norm()).item()
+        flops = 4.0 * B * N * C * C + 4.0 * B * N * nk * C
+        line = f"{name:16s} B={B:3d} N={N:5d} C={C} d={D:3d} norms folded"
+        for a in arms:
+            ts = sorted(res[a])
+            line += f"   {which}={a} {ts[2]:7.1f} us [{ts[0]:.1f}-{ts[-1]:.1f}] ({flops / ts[2] / 1e6:6.1f} TFLOP/s)"
+        print(line + f"   bitwise equal {same}, rel-L2 of the block update {rel:.1e}", flush=True)
+
+
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "--phases":
+    if len(sys.argv) > 1 and sys.argv[1] == "--waves640":
+        ab_arms(sys.argv[1][2:])
+    elif len(sys.argv) > 1 and sys.argv[1] == "--phases":
         phases()
     elif len(sys.argv) > 1 and sys.argv[1] == "--reassoc":
         reassoc()
