@@ -167,9 +167,9 @@ def ab_arms(which):
     from sd_amd._lib import lib
     nk = 77
     assert which == "waves640"
-    arms, setter, reset = (4, 8), lib().sdk_xattn_debug_waves640, 8
+    arms, setter, reset, cw = (4, 8), lib().sdk_xattn_debug_waves640, 8, 640
     for name, B, N, C, D in SHAPES:
-        if (which == "waves640" and C != 640) or not ops.cross_attention_block_supported(C, D, nk, N):
+        if C != cw or not ops.cross_attention_block_supported(C, D, nk, N):
             continue
         H = C // D
         tok = torch.randn(B * N, C, device="cuda").half()
