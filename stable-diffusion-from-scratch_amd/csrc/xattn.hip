@@ -52,28 +52,25 @@ int g_xattn_waves640 = 8;
 typedef _Float16 h4v __attribute__((ext_vector_type(4)));
 typedef __fp16 fp16x4_t __attribute__((ext_vector_type(4)));
 
-constexpr int XQ = 64;     // query rows per workgroup (every form)
+constexpr int XQ = 64;     // query rows per workgroup
 constexpr int XKP = 80;    // key slots (5 blocks of 16)
 
-// NWV waves over QR query rows.  Projections: the waves form NWR = QR / 64 row groups of 64 rows times
-// NWC = NWV / NWR channel groups; wave w owns channels [cg*CW, (cg+1)*CW) of row group rg (cg = w % NWC,
-// rg = w / NWC).  Head phase: RG = QR / 16 groups of 16 query rows, WPR = NWV / RG waves per group, each
-// taking HPI / WPR of an iteration's heads.  Forms:
-//  * 4 waves, 64 rows: one channel quarter per wave (the original form);
-//  * 8 waves, 64 rows at 640 channels: one channel eighth per wave, i.e. the 320-channel form's 80 channels
-//    x 64 rows, whose registers allow 2 waves per SIMD where the 4-wave 640 form holds 512 registers per
-//    lane (one wave per SIMD); the two waves of a 16-row group take one head each;
+// NWV waves over the 64 query rows.  Projections: wave w owns channels [w*CW, (w+1)*CW) of all 64 rows.
+// Head phase: 4 groups of 16 query rows, WPR = NWV / 4 waves per group, each taking HPI / WPR of an
+// iteration's heads.  Forms:
+//  * 4 waves: one channel quarter per wave (320 channels; at 640 the A/B-only form, sdk_xattn_debug_waves640);
+//  * 8 waves at 640 channels: one channel eighth per wave, i.e. the 320-channel form's 80 channels x 64 rows,
+//    whose registers allow 2 waves per SIMD where the 4-wave 640 form holds 512 registers per lane (one wave
+//    per SIMD); the two waves of a 16-row group take one head each.
 //  (a 128-row / 8-wave form at 320 channels — two row halves sharing W fragment fetches and one K / V
 //  staging — measured 5-25 % slower than two 4-wave groups per CU: profiles/r6_xattn_waves640_ab.txt)
-template <int C, int D, int NWV = 4, int QR = 64>
+template <int C, int D, int NWV = 4>
 struct XCfg {
-  static constexpr int XQ = QR;
   static constexpr int NT = 64 * NWV;
   static constexpr int H = C / D;
   static constexpr int DP = (D + 15) / 16 * 16;     // head dim padded to the 16-wide MFMA K / N
-  static constexpr int NWR = QR / 64, NWC = NWV / NWR;
-  static constexpr int RG = QR / 16, WPR = NWV / RG;
-  static constexpr int CW = C / NWC;                // channels per wave in the projections
+  static constexpr int RG = XQ / 16, WPR = NWV / RG;
+  static constexpr int CW = C / NWV;                // channels per wave in the projections
   static constexpr int NB = CW / 16;
   static constexpr int WP = NB <= 5 ? 3 : 4;        // W prefetch depth (K-steps): 80-channel waves keep 2 waves / SIMD
   static constexpr int QLD = C + 8;                 // q / o row stride (halfs); 8 zero pad columns
@@ -90,7 +87,7 @@ struct XCfg {
   static constexpr int LDS_HALFS = XQ * QLD + HPI * KVH;
   static constexpr int LDS_BYTES = LDS_HALFS * 2;
   static_assert(C % 64 == 0 && CW % 16 == 0 && D % 8 == 0 && C % D == 0, "shape");
-  static_assert(QR % 64 == 0 && NWV % NWR == 0 && (WPR == 1 || WPR == 2) && HPI % WPR == 0 && RG <= NWV, "waves");
+  static_assert((NWV == 4 || NWV == 8) && HPI % WPR == 0, "waves");
   static constexpr int GPW = HPI / WPR;             // heads per wave and iteration
   static_assert(DP - D <= 8, "q padding columns cover the last head's d padding");
   static_assert(LDS_BYTES <= 160 * 1024, "LDS");
@@ -187,10 +184,10 @@ struct LnStage {
   }
 };
 
-template <int C, int D, int NWV, int QR>
+template <int C, int D, int NWV>
 __global__ void __launch_bounds__(64 * NWV, 1) xattn_block_kernel(XAttnParams p) {
-  using X = XCfg<C, D, NWV, QR>;
-  constexpr int NT = X::NT, XQ = X::XQ;
+  using X = XCfg<C, D, NWV>;
+  constexpr int NT = X::NT;
   extern __shared__ __attribute__((aligned(16))) half_t xl[];
   half_t* qo = xl;                              // [64][QLD]
   half_t* kvl = qo + XQ * X::QLD;               // HPI x { K [80][KLD], V [80][VLD] }
@@ -198,8 +195,7 @@ __global__ void __launch_bounds__(64 * NWV, 1) xattn_block_kernel(XAttnParams p)
   const int r16 = lane & 15, c16 = lane >> 4;
   const int m0 = blockIdx.x * XQ;
   const int b = m0 / p.n_img;
-  const int n_w = (X::NWR == 1 ? wave : wave % X::NWC) * X::CW;
-  const int prow = X::NWR == 1 ? 0 : (wave / X::NWC) * 64;   // the wave's projection row group
+  const int n_w = wave * X::CW;
 
   static_assert(2 * C * 4 <= X::HPI * X::KVH * 2, "norm gamma / beta staging fits the K / V^T area");
   float* gbl = reinterpret_cast<float*>(kvl);
@@ -229,8 +225,8 @@ __global__ void __launch_bounds__(64 * NWV, 1) xattn_block_kernel(XAttnParams p)
     if (p.ln_in_g) ln2.store(gbl);
   }
   __syncthreads();
-  if (p.ln_in_g) {   // norm2 in place: t = LN(tokens); rows 16w .. 16w + 15 on waves 0 .. RG-1
-    if (wave < X::RG)
+  if (p.ln_in_g) {   // norm2 in place: t = LN(tokens); rows 16w .. 16w + 15 on waves 0-3
+    if (wave < 4)
       ln_quad_rows<C>(qo, X::QLD, gbl, p.ln_in_eps,
                     [&](int row, int c, const h8& v) { *reinterpret_cast<h8*>(qo + row * X::QLD + c) = v; });
     __syncthreads();
@@ -242,7 +238,7 @@ __global__ void __launch_bounds__(64 * NWV, 1) xattn_block_kernel(XAttnParams p)
   stamp(p, 1);
   {
     f4 acc[X::NB][4];
-    proj_wave<C, X::NB, X::WP>(qo + prow * X::QLD, X::QLD, p.wq, n_w, acc);
+    proj_wave<C, X::NB, X::WP>(qo, X::QLD, p.wq, n_w, acc);
     __syncthreads();   // every wave is done reading t
 #pragma unroll
     for (int j = 0; j < X::NB; ++j)
@@ -251,7 +247,7 @@ __global__ void __launch_bounds__(64 * NWV, 1) xattn_block_kernel(XAttnParams p)
         h4v v;
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = (half_t)acc[j][i][r];
-        *reinterpret_cast<h4v*>(qo + (prow + 16 * i + r16) * X::QLD + n_w + 16 * j + 4 * c16) = v;
+        *reinterpret_cast<h4v*>(qo + (16 * i + r16) * X::QLD + n_w + 16 * j + 4 * c16) = v;
       }
   }
   __syncthreads();
@@ -262,9 +258,9 @@ __global__ void __launch_bounds__(64 * NWV, 1) xattn_block_kernel(XAttnParams p)
   // iterations' heads are loaded into registers KVA iterations ahead and written to LDS after
   // the current iteration's closing barrier.
   const half_t* kvb = p.kv + (size_t)b * p.nk * p.kv_ld;
-  const int qrow = 16 * (X::WPR == 1 ? wave : wave % X::RG) + r16;   // this lane's query (S^T column)
+  const int qrow = 16 * (NWV == 4 ? wave : wave & 3) + r16;   // this lane's query (S^T column)
   constexpr int HPI = X::HPI, GPW = X::GPW;
-  const int g0 = X::WPR == 1 ? 0 : (wave / X::RG) * GPW;            // the wave's first head slot of an iteration
+  const int g0 = NWV == 4 ? 0 : (wave >> 2) * GPW;            // the wave's first head slot of an iteration
   constexpr int CH = D / 8;                     // 16-B chunks per key row
   constexpr int NCH = (XKP * CH + NT - 1) / NT; // chunks per thread per head
   constexpr int NIT = (X::H + HPI - 1) / HPI;
@@ -411,7 +407,7 @@ __global__ void __launch_bounds__(64 * NWV, 1) xattn_block_kernel(XAttnParams p)
     LnStage<C, NT> ln3;
     if (p.out_ln) ln3.load(p.ln_out_g, p.ln_out_b);
     f4 acc[X::NB][4];
-    proj_wave<C, X::NB, X::WP>(qo + prow * X::QLD, X::QLD, p.wo, n_w, acc);
+    proj_wave<C, X::NB, X::WP>(qo, X::QLD, p.wo, n_w, acc);
     __syncthreads();   // every wave is done reading o
     stamp(p, 4);
 #pragma unroll
@@ -425,7 +421,7 @@ __global__ void __launch_bounds__(64 * NWV, 1) xattn_block_kernel(XAttnParams p)
         h4v v;
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = (half_t)(acc[j][i][r] + bv[r]);
-        *reinterpret_cast<h4v*>(qo + (prow + 16 * i + r16) * X::QLD + n) = v;
+        *reinterpret_cast<h4v*>(qo + (16 * i + r16) * X::QLD + n) = v;
       }
     }
     if (p.out_ln) ln3.store(gbl);   // phase B is over: the K / V^T area is free
@@ -447,7 +443,7 @@ __global__ void __launch_bounds__(64 * NWV, 1) xattn_block_kernel(XAttnParams p)
       __syncthreads();
       half_t* dst = p.out_ln + (size_t)m0 * p.out_ln_ld;
       const int ld = p.out_ln_ld;
-      if (wave < X::RG)
+      if (wave < 4)
         ln_quad_rows<C>(qo, X::QLD, gbl, p.ln_out_eps,
                       [&](int row, int c, const h8& v) { *reinterpret_cast<h8*>(dst + (size_t)row * ld + c) = v; });
     }
@@ -455,14 +451,13 @@ __global__ void __launch_bounds__(64 * NWV, 1) xattn_block_kernel(XAttnParams p)
   stamp(p, 5);
 }
 
-template <int C, int D, int NWV = 4, int QR = 64>
+template <int C, int D, int NWV = 4>
 int launch_xattn(const XAttnParams& p, int m, hipStream_t s) {
-  using X = XCfg<C, D, NWV, QR>;
+  using X = XCfg<C, D, NWV>;
   static std::atomic<unsigned long long> attr{0};
-  if (int e = ensure_dyn_lds((const void*)xattn_block_kernel<C, D, NWV, QR>, X::LDS_BYTES, attr,
-                             "cross_attention_block"))
+  if (int e = ensure_dyn_lds((const void*)xattn_block_kernel<C, D, NWV>, X::LDS_BYTES, attr, "cross_attention_block"))
     return e;
-  hipLaunchKernelGGL((xattn_block_kernel<C, D, NWV, QR>), dim3(m / X::XQ), dim3(X::NT), X::LDS_BYTES, s, p);
+  hipLaunchKernelGGL((xattn_block_kernel<C, D, NWV>), dim3(m / XQ), dim3(X::NT), X::LDS_BYTES, s, p);
   return check_launch("xattn_block");
 }
 
