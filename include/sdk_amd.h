@@ -241,7 +241,9 @@ int sdk_attention(const sdk_attention_args* a, sdk_stream_t stream);
  * (openai_model/attention.py:63-117) and the residual add of BasicTransformerBlock
  * (attention.py:249).  t / res / out: [batch*n_img, ld] fp16; kv: [batch*nk, kv_ld] fp16
  * with K at columns [0, channels) and V at [channels, 2*channels); wq / wo: fp16 [>= channels
- * rows][w_ld = channels] (row n = output channel); bias fp32 [channels] or NULL.
+ * rows][w_ld = channels] (row n = output channel), or w_ld = 0: both in the fragment-packed layout of
+ * sdk_xattn_pack_weight (channels * channels fp16, one contiguous KiB per MFMA fragment: whole-line weight
+ * fetches); bias fp32 [channels] or NULL.
  * Shapes: sdk_cross_attention_block_supported() (channels 320 / 640, head_dim 40 / 64 / 80,
  * nk <= 80, n_img % 64 == 0); others return SDK_EINVAL (callers use the three-launch path).
  */
@@ -254,6 +256,9 @@ typedef struct {
 } sdk_xattn_args;
 
 int sdk_cross_attention_block_supported(int32_t channels, int32_t head_dim, int32_t nk, int32_t n_img);
+/* One-time pack of a projection weight (fp16 [channels rows][w_ld], nn.Linear layout) into packed
+ * (channels * channels fp16, 16-B aligned, device) for sdk_xattn_args.w_ld = 0; channels 320 / 640. */
+int sdk_xattn_pack_weight(const void* w, int32_t w_ld, void* packed, int32_t channels, sdk_stream_t stream);
 int sdk_cross_attention_block(const sdk_xattn_args* a, sdk_stream_t stream);
 
 /* The same block with BasicTransformerBlock's two LayerNorms around it fused in

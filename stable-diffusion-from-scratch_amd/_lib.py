@@ -82,7 +82,7 @@ OUT_NHWC_F16, OUT_NCHW_F32, OUT_GEGLU_F16, OUT_ROWS_F32 = 0, 1, 2, 3
 ACT_NONE, ACT_QUICK_GELU = 0, 1
 
 EXPORTS = ["sdk_conv2d_plan", "sdk_conv2d", "sdk_group_norm_workspace", "sdk_group_norm_affine", "sdk_group_norm_apply", "sdk_group_norm_apply_padded", "sdk_group_norm_apply_ex", "sdk_group_norm", "sdk_group_norm_finalize", "sdk_layer_norm",
-           "sdk_attention", "sdk_cross_attention_block_supported", "sdk_cross_attention_block", "sdk_cross_attention_block_ln", "sdk_segment_softmax", "sdk_ff_supported", "sdk_ff_packed_bytes", "sdk_ff_pack", "sdk_feed_forward", "sdk_token_linear_supported", "sdk_token_linear", "sdk_token_linear_ln", "sdk_ddim_step", "sdk_ddpm_step", "sdk_timestep_embedding", "sdk_nchw_to_nhwc",
+           "sdk_attention", "sdk_cross_attention_block_supported", "sdk_xattn_pack_weight", "sdk_cross_attention_block", "sdk_cross_attention_block_ln", "sdk_segment_softmax", "sdk_ff_supported", "sdk_ff_packed_bytes", "sdk_ff_pack", "sdk_feed_forward", "sdk_token_linear_supported", "sdk_token_linear", "sdk_token_linear_ln", "sdk_ddim_step", "sdk_ddpm_step", "sdk_timestep_embedding", "sdk_nchw_to_nhwc",
            "sdk_diag_gaussian_sample", "sdk_stochastic_encode", "sdk_token_embedding", "sdk_extract_patches",
            "sdk_fold_patches", "sdk_upsample_bilinear2x", "sdk_upsample_nearest2x_padded", "sdk_gelu", "sdk_last_error", "sdk_version", "sdk_kernel_name",
            "sdk_probe_mfma_flops", "sdk_probe_mfma", "sdk_probe_copy", "sdk_probe_copy_ex"]
@@ -117,6 +117,7 @@ def lib():
     L.sdk_layer_norm.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp, f32, vp]
     L.sdk_attention.argtypes = [C.POINTER(AttentionArgs), vp]
     L.sdk_cross_attention_block_supported.argtypes = [i32, i32, i32, i32]
+    L.sdk_xattn_pack_weight.argtypes = [vp, i32, vp, i32, vp]
     L.sdk_cross_attention_block.argtypes = [C.POINTER(XAttnArgs), vp]
     L.sdk_cross_attention_block_ln.argtypes = [C.POINTER(XAttnArgs), C.POINTER(XAttnLnArgs), vp]
     L.sdk_segment_softmax.argtypes = [vp, i32, vp, i32, i32, i32, i32, f32, vp]

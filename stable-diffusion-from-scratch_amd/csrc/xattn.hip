@@ -98,7 +98,16 @@ struct XCfg {
 // every workgroup).  K-steps of 32, fully unrolled.  The W fragments are the long-latency operand:
 // they run WP K-steps ahead through a ring of WP + 1 register sets (the phase was L2-latency-bound
 // at two steps ahead: 13 us for 1.3 us of MFMAs); the LDS fragments run one step ahead.
-template <int C, int NB, int WP>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t xattn_rsrc(const void* base, long long bytes) {
+  const uint64_t a = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  const int n = __builtin_amdgcn_readfirstlane((int)bytes);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
+}
+
+// PK: W in the fragment-packed layout of sdk_xattn_pack_weight — the 64 lanes' 16-B pieces of one (16-channel
+// block, K-step) are 1 KiB contiguous, so a wave-instruction fetches 8 whole 128-B lines instead of 64 B of 16 rows
+template <int C, int NB, int WP, bool PK>
 __device__ __forceinline__ void proj_wave(const half_t* __restrict__ x, int x_ld, const half_t* __restrict__ w,
                                           int n_w, f4 (&acc)[NB][4]) {
   const int lane = threadIdx.x & 63, r16 = lane & 15, c16 = lane >> 4;
@@ -106,14 +115,22 @@ __device__ __forceinline__ void proj_wave(const half_t* __restrict__ x, int x_ld
   for (int j = 0; j < NB; ++j)
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[j][i] = f4{};
-  const half_t* wp = w + (size_t)(n_w + r16) * C + 8 * c16;
-  const half_t* xp = x + (size_t)r16 * x_ld + 8 * c16;
   constexpr int KS = C / 32;
+  const half_t* wp = w + (size_t)(n_w + r16) * C + 8 * c16;
+  // packed: one buffer descriptor over the wave's NB x KS KiB pieces, the lane's 16 B as the only VGPR offset and
+  // the piece as the scalar offset (no per-block 64-bit pointers)
+  const __amdgpu_buffer_rsrc_t wr = xattn_rsrc(w + (size_t)(n_w / 16) * KS * 512, (long long)NB * KS * 1024);
+  const half_t* xp = x + (size_t)r16 * x_ld + 8 * c16;
   constexpr int WR = WP + 1;
   h8 fw[WR][NB], fx[2][4];
   auto load_w = [&](int ks) {
 #pragma unroll
-    for (int j = 0; j < NB; ++j) fw[ks % WR][j] = *reinterpret_cast<const h8*>(wp + (size_t)j * 16 * C + 32 * ks);
+    for (int j = 0; j < NB; ++j) {
+      if constexpr (PK)
+        fw[ks % WR][j] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, lane * 16, (j * KS + ks) * 1024, 0));
+      else
+        fw[ks % WR][j] = *reinterpret_cast<const h8*>(wp + (size_t)j * 16 * C + 32 * ks);
+    }
   };
   auto load_x = [&](int ks) {
 #pragma unroll
@@ -184,8 +201,10 @@ struct LnStage {
   }
 };
 
-template <int C, int D, int NWV>
-__global__ void __launch_bounds__(64 * NWV, 1) xattn_block_kernel(XAttnParams p) {
+// the packed 320-channel form is held to 2 waves per SIMD (two groups per CU) explicitly: left alone hipcc spends
+// 262 registers on it
+template <int C, int D, int NWV, bool PK>
+__global__ void __launch_bounds__(64 * NWV, PK && C <= 320 ? 2 : 1) xattn_block_kernel(XAttnParams p) {
   using X = XCfg<C, D, NWV>;
   constexpr int NT = X::NT;
   extern __shared__ __attribute__((aligned(16))) half_t xl[];
@@ -238,7 +257,7 @@ __global__ void __launch_bounds__(64 * NWV, 1) xattn_block_kernel(XAttnParams p)
   stamp(p, 1);
   {
     f4 acc[X::NB][4];
-    proj_wave<C, X::NB, X::WP>(qo, X::QLD, p.wq, n_w, acc);
+    proj_wave<C, X::NB, X::WP, PK>(qo, X::QLD, p.wq, n_w, acc);
     __syncthreads();   // every wave is done reading t
 #pragma unroll
     for (int j = 0; j < X::NB; ++j)
@@ -407,7 +426,7 @@ __global__ void __launch_bounds__(64 * NWV, 1) xattn_block_kernel(XAttnParams p)
     LnStage<C, NT> ln3;
     if (p.out_ln) ln3.load(p.ln_out_g, p.ln_out_b);
     f4 acc[X::NB][4];
-    proj_wave<C, X::NB, X::WP>(qo, X::QLD, p.wo, n_w, acc);
+    proj_wave<C, X::NB, X::WP, PK>(qo, X::QLD, p.wo, n_w, acc);
     __syncthreads();   // every wave is done reading o
     stamp(p, 4);
 #pragma unroll
@@ -451,14 +470,31 @@ __global__ void __launch_bounds__(64 * NWV, 1) xattn_block_kernel(XAttnParams p)
   stamp(p, 5);
 }
 
-template <int C, int D, int NWV = 4>
-int launch_xattn(const XAttnParams& p, int m, hipStream_t s) {
+template <int C, int D, int NWV, bool PK>
+int launch_xattn2(const XAttnParams& p, int m, hipStream_t s) {
   using X = XCfg<C, D, NWV>;
   static std::atomic<unsigned long long> attr{0};
-  if (int e = ensure_dyn_lds((const void*)xattn_block_kernel<C, D, NWV>, X::LDS_BYTES, attr, "cross_attention_block"))
+  if (int e = ensure_dyn_lds((const void*)xattn_block_kernel<C, D, NWV, PK>, X::LDS_BYTES, attr, "cross_attention_block"))
     return e;
-  hipLaunchKernelGGL((xattn_block_kernel<C, D, NWV>), dim3(m / XQ), dim3(X::NT), X::LDS_BYTES, s, p);
+  hipLaunchKernelGGL((xattn_block_kernel<C, D, NWV, PK>), dim3(m / XQ), dim3(X::NT), X::LDS_BYTES, s, p);
   return check_launch("xattn_block");
+}
+
+template <int C, int D, int NWV = 4>
+int launch_xattn(const XAttnParams& p, int m, bool packed, hipStream_t s) {
+  return packed ? launch_xattn2<C, D, NWV, true>(p, m, s) : launch_xattn2<C, D, NWV, false>(p, m, s);
+}
+
+// fragment-packed copy of a [C][w_ld] fp16 projection weight: piece ((nb * KS + ks) * 64 + lane) holds row
+// 16 nb + (lane & 15), columns 32 ks + 8 (lane >> 4) .. + 7 (the A-fragment of v_mfma_f32_16x16x32_f16)
+__global__ void __launch_bounds__(256) xattn_pack_kernel(const half_t* __restrict__ w, int w_ld, half_t* __restrict__ pk,
+                                                         int C) {
+  const int e = blockIdx.x * 256 + threadIdx.x;     // 16-B piece
+  if (e >= C * C / 8) return;
+  const int lane = e & 63, f = e >> 6, ks_n = C / 32;
+  const int nb = f / ks_n, ks = f - nb * ks_n;
+  *reinterpret_cast<h8*>(pk + (size_t)e * 8) =
+      *reinterpret_cast<const h8*>(w + (size_t)(16 * nb + (lane & 15)) * w_ld + 32 * ks + 8 * (lane >> 4));
 }
 
 // Segment softmax of the reassociated cross-attention (1280-channel levels, attention.py:106-112
@@ -526,7 +562,9 @@ int xattn_run(const sdk_xattn_args* a, const sdk_xattn_ln_args* ln, sdk_stream_t
   if (a->batch <= 0) return fail(SDK_EINVAL, "cross_attention_block: empty batch");
   if (a->t_ld % 8 || a->kv_ld % 8 || a->out_ld % 8 || (a->res && a->res_ld % 8) || a->kv_ld < 2 * a->channels)
     return fail(SDK_EINVAL, "cross_attention_block: row strides must be multiples of 8 (kv >= 2*channels)");
-  if (a->w_ld != a->channels) return fail(SDK_EINVAL, "cross_attention_block: weight rows must be channels long");
+  if (a->w_ld != a->channels && a->w_ld != 0)
+    return fail(SDK_EINVAL, "cross_attention_block: w_ld must be channels (row layout) or 0 (sdk_xattn_pack_weight layout)");
+  const bool packed = a->w_ld == 0;
   XAttnParams p{};
   p.t = (const half_t*)a->t; p.kv = (const half_t*)a->kv; p.wq = (const half_t*)a->wq; p.wo = (const half_t*)a->wo;
   p.bo = a->bias; p.res = (const half_t*)a->res; p.out = (half_t*)a->out;
@@ -550,12 +588,24 @@ int xattn_run(const sdk_xattn_args* a, const sdk_xattn_ln_args* ln, sdk_stream_t
   }
   const int m = a->batch * a->n_img;
   hipStream_t s = (hipStream_t)stream;
-  if (a->channels == 320) return a->head_dim == 40 ? launch_xattn<320, 40>(p, m, s) : launch_xattn<320, 64>(p, m, s);
+  if (a->channels == 320)
+    return a->head_dim == 40 ? launch_xattn<320, 40>(p, m, packed, s) : launch_xattn<320, 64>(p, m, packed, s);
   if (g_xattn_waves640 == 4)
-    return a->head_dim == 80 ? launch_xattn<640, 80, 4>(p, m, s) : launch_xattn<640, 64, 4>(p, m, s);
-  return a->head_dim == 80 ? launch_xattn<640, 80, 8>(p, m, s) : launch_xattn<640, 64, 8>(p, m, s);
+    return a->head_dim == 80 ? launch_xattn<640, 80, 4>(p, m, packed, s) : launch_xattn<640, 64, 4>(p, m, packed, s);
+  return a->head_dim == 80 ? launch_xattn<640, 80, 8>(p, m, packed, s) : launch_xattn<640, 64, 8>(p, m, packed, s);
 }
 }  // namespace
+
+extern "C" int sdk_xattn_pack_weight(const void* w, int32_t w_ld, void* packed, int32_t channels, sdk_stream_t stream) {
+  if (!w || !packed) return fail(SDK_EINVAL, "xattn_pack_weight: null pointer");
+  if (channels != 320 && channels != 640) return fail(SDK_EINVAL, "xattn_pack_weight: channels must be 320 or 640");
+  if (w_ld < channels || w_ld % 8 || (((uintptr_t)w | (uintptr_t)packed) & 15))
+    return fail(SDK_EINVAL, "xattn_pack_weight: w_ld >= channels, w_ld % 8 == 0, 16-B aligned pointers");
+  const int pieces = channels * channels / 8;
+  hipLaunchKernelGGL(xattn_pack_kernel, dim3((pieces + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     (const half_t*)w, w_ld, (half_t*)packed, channels);
+  return check_launch("xattn_pack_weight");
+}
 
 extern "C" int sdk_cross_attention_block(const sdk_xattn_args* a, sdk_stream_t stream) {
   return xattn_run(a, nullptr, stream);

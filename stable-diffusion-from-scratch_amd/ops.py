@@ -865,6 +865,24 @@ def cross_attention_block_supported(channels, head_dim, nk, n_img):
     return bool(lib().sdk_cross_attention_block_supported(channels, head_dim, nk, n_img))
 
 
+# the block's projection weights in the fragment-packed layout (sdk_xattn_pack_weight: whole 128-B lines per weight
+# fetch); False = the row layout (A/B only, same bits)
+XATTN_PACKED_W = False
+
+
+def xattn_packed_weight(pc: PackedConv):
+    """The fragment-packed copy of a channels x channels PackedConv for the cross-attention kernel, made once
+    and kept on the PackedConv (not inside a graph capture: the first eager evaluation makes it)."""
+    pk = getattr(pc, "_xattn_pk", None)
+    if pk is None:
+        Cc = pc.N
+        pk = torch.empty(Cc * Cc, dtype=torch.float16, device=pc.weight.device)
+        check(lib().sdk_xattn_pack_weight(pc.weight.data_ptr(), pc.k_total, pk.data_ptr(), Cc, _stream()),
+              "xattn_pack_weight")
+        pc._xattn_pk = pk
+    return pk
+
+
 def cross_attention_block(t, kv, pc_q: PackedConv, pc_o: PackedConv, *, batch, n_img, nk, heads, head_dim, scale,
                           residual=None, out=None, norm_in=None, norm_out=None, out_ln=None):
     """One-kernel cross-attention block on a cached context K|V: ``to_out(attn(to_q(t), K, V)) + residual``.
@@ -885,10 +903,14 @@ def cross_attention_block(t, kv, pc_q: PackedConv, pc_o: PackedConv, *, batch, n
     _claim(out_ln)
     a = XAttnArgs()
     a.t, a.kv, a.wq, a.wo = t.data_ptr(), kv.data_ptr(), pc_q.weight.data_ptr(), pc_o.weight.data_ptr()
+    packed = XATTN_PACKED_W and (not torch.cuda.is_current_stream_capturing() or
+                                 (hasattr(pc_q, "_xattn_pk") and hasattr(pc_o, "_xattn_pk")))
+    if packed:
+        a.wq, a.wo = xattn_packed_weight(pc_q).data_ptr(), xattn_packed_weight(pc_o).data_ptr()
     a.bias = pc_o.bias.data_ptr() if pc_o.bias is not None else None
     a.res = residual.data_ptr() if residual is not None else None
     a.out = out.data_ptr()
-    a.t_ld, a.kv_ld, a.w_ld = t.stride(0), kv.stride(0), Cc
+    a.t_ld, a.kv_ld, a.w_ld = t.stride(0), kv.stride(0), 0 if packed else Cc
     a.res_ld = residual.stride(0) if residual is not None else 0
     a.out_ld = out.stride(0)
     a.batch, a.n_img, a.nk, a.channels, a.head_dim, a.scale = batch, n_img, nk, Cc, head_dim, scale

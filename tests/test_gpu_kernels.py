@@ -542,6 +542,50 @@ def test_cross_attention_block_640_waves_bitwise(ops, B, N, D, nk):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("B,N,C,D,nk", [(2, 4096, 320, 40, 77), (2, 1024, 640, 80, 77), (1, 256, 320, 64, 77),
+                                        (2, 64, 640, 64, 80), (3, 192, 320, 40, 13)])
+def test_cross_attention_block_packed_weights_bitwise(ops, B, N, C, D, nk):
+    """Projection weights in the fragment-packed layout (sdk_xattn_pack_weight, w_ld = 0; the default) and in
+    the row layout (w_ld = channels) give the same bits, with and without the folded norms."""
+    g = torch.Generator(device="cpu").manual_seed(17 * N + C + nk)
+    tok = (torch.randn(B * N, C, generator=g) * 2 + 0.5).half().to(DEV)
+    kv = torch.randn(B * nk, 2 * C, generator=g).half().to(DEV)
+    pcq = ops.PackedConv([(torch.randn(C, C, generator=g) / math.sqrt(C), C)], None, device=DEV)
+    pco = ops.PackedConv([(torch.randn(C, C, generator=g) / math.sqrt(C), C)], torch.randn(C, generator=g) * 0.1,
+                         device=DEV)
+    gg, bb = (1 + 0.1 * torch.randn(C, generator=g)).to(DEV), (0.1 * torch.randn(C, generator=g)).to(DEV)
+    kw = dict(batch=B, n_img=N, nk=nk, heads=C // D, head_dim=D, scale=D ** -0.5, residual=tok)
+    old = ops.XATTN_PACKED_W
+    outs = {}
+    try:
+        for packed in (False, True):
+            ops.XATTN_PACKED_W = packed
+            y = ops.cross_attention_block(tok, kv, pcq, pco, **kw)
+            yn, t3 = ops.cross_attention_block(tok, kv, pcq, pco, norm_in=(gg, bb, 1e-5), norm_out=(gg, bb, 1e-5), **kw)
+            torch.cuda.synchronize()
+            outs[packed] = (y, yn, t3)
+    finally:
+        ops.XATTN_PACKED_W = old
+    assert hasattr(pcq, "_xattn_pk") and pcq._xattn_pk.numel() == C * C
+    for a_, b_ in zip(outs[False], outs[True]):
+        assert torch.equal(a_, b_)
+
+
+def test_xattn_pack_weight_layout_and_rejects(ops, sdk):
+    """The packed layout: piece ((nb * C/32 + ks) * 64 + lane) = W[16 nb + lane % 16, 32 ks + 8 (lane // 16) : +8];
+    bad shapes / strides are refused."""
+    from sd_amd import _lib
+    C = 320
+    w = torch.randn(C, C + 8).half().to(DEV)
+    pk = torch.empty(C * C, dtype=torch.float16, device=DEV)
+    assert _lib.lib().sdk_xattn_pack_weight(w.data_ptr(), C + 8, pk.data_ptr(), C, None) == 0
+    torch.cuda.synchronize()
+    ref = w[:, :C].cpu().view(C // 16, 16, C // 32, 4, 8).permute(0, 2, 3, 1, 4).reshape(-1)
+    assert torch.equal(pk.cpu(), ref)
+    assert _lib.lib().sdk_xattn_pack_weight(w.data_ptr(), C + 8, pk.data_ptr(), 1280, None) != 0
+    assert _lib.lib().sdk_xattn_pack_weight(w.data_ptr(), C - 8, pk.data_ptr(), C, None) != 0
+
+
 def test_cross_attention_block_fused_norms_rejects(ops):
     C, D, N, nk = 320, 40, 64, 77
     t = torch.zeros(N, C, dtype=torch.float16, device=DEV)

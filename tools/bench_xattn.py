@@ -158,7 +158,8 @@ def reassoc():
 
 def ab_arms(which):
     """The block with the norms folded (the UNet's form), A/B of two kernel settings in one process:
-    ``waves640`` = 4 vs 8 waves per workgroup at 640 channels (sdk_xattn_debug_waves640; bitwise equal).
+    ``waves640`` = 4 vs 8 waves per workgroup at 640 channels (sdk_xattn_debug_waves640; bitwise equal),
+    ``packed`` = projection weights in the row layout vs fragment-packed (ops.XATTN_PACKED_W; bitwise equal).
     5 alternating rounds of 20 launches each, median [min-max] per arm, bitwise check and rel-L2 of the
     block update."""
     import sd_amd_loader
@@ -166,10 +167,12 @@ def ab_arms(which):
     from sd_amd import ops
     from sd_amd._lib import lib
     nk = 77
-    assert which == "waves640"
-    arms, setter, reset, cw = (4, 8), lib().sdk_xattn_debug_waves640, 8, 640
+    if which == "waves640":
+        arms, setter, reset, cw = (4, 8), lib().sdk_xattn_debug_waves640, 8, 640
+    else:
+        arms, setter, reset, cw = (0, 1), lambda v: setattr(ops, "XATTN_PACKED_W", bool(v)), 1, None
     for name, B, N, C, D in SHAPES:
-        if C != cw or not ops.cross_attention_block_supported(C, D, nk, N):
+        if (cw is not None and C != cw) or not ops.cross_attention_block_supported(C, D, nk, N):
             continue
         H = C // D
         tok = torch.randn(B * N, C, device="cuda").half()
@@ -203,7 +206,7 @@ def ab_arms(which):
 
 
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "--waves640":
+    if len(sys.argv) > 1 and sys.argv[1] in ("--waves640", "--packed"):
         ab_arms(sys.argv[1][2:])
     elif len(sys.argv) > 1 and sys.argv[1] == "--phases":
         phases()
