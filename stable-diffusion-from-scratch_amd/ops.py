@@ -867,7 +867,7 @@ def cross_attention_block_supported(channels, head_dim, nk, n_img):
 
 # the block's projection weights in the fragment-packed layout (sdk_xattn_pack_weight: whole 128-B lines per weight
 # fetch); False = the row layout (A/B only, same bits)
-XATTN_PACKED_W = False
+XATTN_PACKED_W = True
 
 
 def xattn_packed_weight(pc: PackedConv):
