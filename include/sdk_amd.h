@@ -243,8 +243,7 @@ int sdk_attention(const sdk_attention_args* a, sdk_stream_t stream);
  * with K at columns [0, channels) and V at [channels, 2*channels); wq / wo: fp16 [>= channels
  * rows][w_ld = channels] (row n = output channel), or w_ld = 0: both in the fragment-packed layout of
  * sdk_xattn_pack_weight (channels * channels fp16, one contiguous KiB per MFMA fragment: whole-line weight
- * fetches); bias fp32 [channels] or NULL.  kv_ld = 0 (with w_ld = 0): kv is head-packed, fp16
- * [batch][channels / head_dim][K, V][80][head_dim] with keys >= nk zero (one contiguous run per head).
+ * fetches); bias fp32 [channels] or NULL.
  * Shapes: sdk_cross_attention_block_supported() (channels 320 / 640, head_dim 40 / 64 / 80,
  * nk <= 80, n_img % 64 == 0); others return SDK_EINVAL (callers use the three-launch path).
  */

@@ -203,9 +203,7 @@ struct LnStage {
 
 // the packed 320-channel form is held to 2 waves per SIMD (two groups per CU) explicitly: left alone hipcc spends
 // 262 registers on it
-// PK bit 0: Wq / Wo fragment-packed (w_ld = 0); bit 1: the context K|V head-packed (kv_ld = 0: [batch][head][K, V][80
-// keys][head_dim], keys >= nk zero — each head's 80-160-B key rows become one contiguous run)
-template <int C, int D, int NWV, int PK>
+template <int C, int D, int NWV, bool PK>
 __global__ void __launch_bounds__(64 * NWV, PK && C <= 320 ? 2 : 1) xattn_block_kernel(XAttnParams p) {
   using X = XCfg<C, D, NWV>;
   constexpr int NT = X::NT;
@@ -259,7 +257,7 @@ __global__ void __launch_bounds__(64 * NWV, PK && C <= 320 ? 2 : 1) xattn_block_
   stamp(p, 1);
   {
     f4 acc[X::NB][4];
-    proj_wave<C, X::NB, X::WP, (PK & 1) != 0>(qo, X::QLD, p.wq, n_w, acc);
+    proj_wave<C, X::NB, X::WP, PK>(qo, X::QLD, p.wq, n_w, acc);
     __syncthreads();   // every wave is done reading t
 #pragma unroll
     for (int j = 0; j < X::NB; ++j)
@@ -278,7 +276,7 @@ __global__ void __launch_bounds__(64 * NWV, PK && C <= 320 ? 2 : 1) xattn_block_
   // exact softmax over <= 80 keys; o_h overwrites q_h in LDS.  The K / V chunks (16 B) of later
   // iterations' heads are loaded into registers KVA iterations ahead and written to LDS after
   // the current iteration's closing barrier.
-  const half_t* kvb = (PK & 2) ? p.kv + (size_t)b * X::H * 2 * XKP * D : p.kv + (size_t)b * p.nk * p.kv_ld;
+  const half_t* kvb = p.kv + (size_t)b * p.nk * p.kv_ld;
   const int qrow = 16 * (NWV == 4 ? wave : wave & 3) + r16;   // this lane's query (S^T column)
   constexpr int HPI = X::HPI, GPW = X::GPW;
   const int g0 = NWV == 4 ? 0 : (wave >> 2) * GPW;            // the wave's first head slot of an iteration
@@ -296,10 +294,9 @@ __global__ void __launch_bounds__(64 * NWV, PK && C <= 320 ? 2 : 1) xattn_block_
         const int e = tid + NT * u;
         const int key = e / CH, ch = e - key * CH;
         if (key < p.nk && h < X::H) {
-          const half_t* src = (PK & 2) ? kvb + (size_t)(h * 2 * XKP + key) * D + 8 * ch
-                                       : kvb + (size_t)key * p.kv_ld + h * D + 8 * ch;
+          const half_t* src = kvb + (size_t)key * p.kv_ld + h * D + 8 * ch;
           rk[sl][g][u] = *reinterpret_cast<const h8*>(src);
-          rv[sl][g][u] = *reinterpret_cast<const h8*>(src + ((PK & 2) ? XKP * D : C));
+          rv[sl][g][u] = *reinterpret_cast<const h8*>(src + C);
         }
       }
     }
@@ -429,7 +426,7 @@ __global__ void __launch_bounds__(64 * NWV, PK && C <= 320 ? 2 : 1) xattn_block_
     LnStage<C, NT> ln3;
     if (p.out_ln) ln3.load(p.ln_out_g, p.ln_out_b);
     f4 acc[X::NB][4];
-    proj_wave<C, X::NB, X::WP, (PK & 1) != 0>(qo, X::QLD, p.wo, n_w, acc);
+    proj_wave<C, X::NB, X::WP, PK>(qo, X::QLD, p.wo, n_w, acc);
     __syncthreads();   // every wave is done reading o
     stamp(p, 4);
 #pragma unroll
@@ -473,7 +470,7 @@ __global__ void __launch_bounds__(64 * NWV, PK && C <= 320 ? 2 : 1) xattn_block_
   stamp(p, 5);
 }
 
-template <int C, int D, int NWV, int PK>
+template <int C, int D, int NWV, bool PK>
 int launch_xattn2(const XAttnParams& p, int m, hipStream_t s) {
   using X = XCfg<C, D, NWV>;
   static std::atomic<unsigned long long> attr{0};
@@ -484,9 +481,8 @@ int launch_xattn2(const XAttnParams& p, int m, hipStream_t s) {
 }
 
 template <int C, int D, int NWV = 4>
-int launch_xattn(const XAttnParams& p, int m, int packed, hipStream_t s) {
-  return packed == 3 ? launch_xattn2<C, D, NWV, 3>(p, m, s)
-         : packed ? launch_xattn2<C, D, NWV, 1>(p, m, s) : launch_xattn2<C, D, NWV, 0>(p, m, s);
+int launch_xattn(const XAttnParams& p, int m, bool packed, hipStream_t s) {
+  return packed ? launch_xattn2<C, D, NWV, true>(p, m, s) : launch_xattn2<C, D, NWV, false>(p, m, s);
 }
 
 // fragment-packed copy of a [C][w_ld] fp16 projection weight: piece ((nb * KS + ks) * 64 + lane) holds row
@@ -564,14 +560,11 @@ int xattn_run(const sdk_xattn_args* a, const sdk_xattn_ln_args* ln, sdk_stream_t
     return fail(SDK_EINVAL, "cross_attention_block: unsupported shape (channels 320/640, head_dim 40/64/80, "
                             "nk <= 80, tokens per image a multiple of 64)");
   if (a->batch <= 0) return fail(SDK_EINVAL, "cross_attention_block: empty batch");
-  if (a->t_ld % 8 || a->kv_ld % 8 || a->out_ld % 8 || (a->res && a->res_ld % 8) ||
-      (a->kv_ld != 0 && a->kv_ld < 2 * a->channels))
-    return fail(SDK_EINVAL, "cross_attention_block: row strides must be multiples of 8 (kv >= 2*channels, or 0: head-packed)");
+  if (a->t_ld % 8 || a->kv_ld % 8 || a->out_ld % 8 || (a->res && a->res_ld % 8) || a->kv_ld < 2 * a->channels)
+    return fail(SDK_EINVAL, "cross_attention_block: row strides must be multiples of 8 (kv >= 2*channels)");
   if (a->w_ld != a->channels && a->w_ld != 0)
     return fail(SDK_EINVAL, "cross_attention_block: w_ld must be channels (row layout) or 0 (sdk_xattn_pack_weight layout)");
-  if (a->kv_ld == 0 && a->w_ld != 0)
-    return fail(SDK_EINVAL, "cross_attention_block: head-packed K|V (kv_ld = 0) needs packed weights (w_ld = 0)");
-  const int packed = a->kv_ld == 0 ? 3 : a->w_ld == 0 ? 1 : 0;
+  const bool packed = a->w_ld == 0;
   XAttnParams p{};
   p.t = (const half_t*)a->t; p.kv = (const half_t*)a->kv; p.wq = (const half_t*)a->wq; p.wo = (const half_t*)a->wo;
   p.bo = a->bias; p.res = (const half_t*)a->res; p.out = (half_t*)a->out;

@@ -883,23 +883,6 @@ def xattn_packed_weight(pc: PackedConv):
     return pk
 
 
-# the cached context K|V head-packed for the block (kv_ld = 0; needs XATTN_PACKED_W): each head's key rows one
-# contiguous run; False = the context rows as the K|V GEMM stored them (A/B only, same bits)
-XATTN_PACKED_KV = False
-
-
-def xattn_packed_kv(kv, batch, nk, heads, head_dim):
-    """[batch][heads][K, V][80][head_dim] fp16 copy of a context K|V [batch*nk, >= 2*heads*head_dim] (keys >= nk
-    zero), made once per conditioning tensor and kept on it (the first eager evaluation makes it)."""
-    pk = getattr(kv, "_xattn_kvp", None)
-    if pk is None or pk.shape[:2] != (batch, heads):
-        Cc = heads * head_dim
-        pk = torch.zeros(batch, heads, 2, 80, head_dim, dtype=torch.float16, device=kv.device)
-        pk[:, :, :, :nk] = kv[:, :2 * Cc].reshape(batch, nk, 2, heads, head_dim).permute(0, 3, 2, 1, 4)
-        kv._xattn_kvp = pk
-    return pk
-
-
 def cross_attention_block(t, kv, pc_q: PackedConv, pc_o: PackedConv, *, batch, n_img, nk, heads, head_dim, scale,
                           residual=None, out=None, norm_in=None, norm_out=None, out_ln=None):
     """One-kernel cross-attention block on a cached context K|V: ``to_out(attn(to_q(t), K, V)) + residual``.
@@ -924,14 +907,10 @@ def cross_attention_block(t, kv, pc_q: PackedConv, pc_o: PackedConv, *, batch, n
                                  (hasattr(pc_q, "_xattn_pk") and hasattr(pc_o, "_xattn_pk")))
     if packed:
         a.wq, a.wo = xattn_packed_weight(pc_q).data_ptr(), xattn_packed_weight(pc_o).data_ptr()
-    packed_kv = packed and XATTN_PACKED_KV and nk <= 80 and (not torch.cuda.is_current_stream_capturing() or
-                                                             hasattr(kv, "_xattn_kvp"))
-    if packed_kv:
-        a.kv = xattn_packed_kv(kv, batch, nk, heads, head_dim).data_ptr()
     a.bias = pc_o.bias.data_ptr() if pc_o.bias is not None else None
     a.res = residual.data_ptr() if residual is not None else None
     a.out = out.data_ptr()
-    a.t_ld, a.kv_ld, a.w_ld = t.stride(0), 0 if packed_kv else kv.stride(0), 0 if packed else Cc
+    a.t_ld, a.kv_ld, a.w_ld = t.stride(0), kv.stride(0), 0 if packed else Cc
     a.res_ld = residual.stride(0) if residual is not None else 0
     a.out_ld = out.stride(0)
     a.batch, a.n_img, a.nk, a.channels, a.head_dim, a.scale = batch, n_img, nk, Cc, head_dim, scale

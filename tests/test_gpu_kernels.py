@@ -571,37 +571,6 @@ def test_cross_attention_block_packed_weights_bitwise(ops, B, N, C, D, nk):
         assert torch.equal(a_, b_)
 
 
-@pytest.mark.parametrize("B,N,C,D,nk", [(2, 4096, 320, 40, 77), (2, 1024, 640, 80, 77), (1, 256, 320, 64, 77),
-                                        (2, 64, 640, 64, 80), (3, 192, 320, 40, 13)])
-def test_cross_attention_block_packed_kv_bitwise(ops, B, N, C, D, nk):
-    """The context K|V head-packed (kv_ld = 0, ops.XATTN_PACKED_KV) gives the same bits as the context rows,
-    with and without the folded norms; the packed copy is made once per K|V tensor."""
-    g = torch.Generator(device="cpu").manual_seed(19 * N + C + nk)
-    tok = (torch.randn(B * N, C, generator=g) * 2 + 0.5).half().to(DEV)
-    kv = torch.randn(B * nk, 2 * C, generator=g).half().to(DEV)
-    pcq = ops.PackedConv([(torch.randn(C, C, generator=g) / math.sqrt(C), C)], None, device=DEV)
-    pco = ops.PackedConv([(torch.randn(C, C, generator=g) / math.sqrt(C), C)], torch.randn(C, generator=g) * 0.1,
-                         device=DEV)
-    gg, bb = (1 + 0.1 * torch.randn(C, generator=g)).to(DEV), (0.1 * torch.randn(C, generator=g)).to(DEV)
-    kw = dict(batch=B, n_img=N, nk=nk, heads=C // D, head_dim=D, scale=D ** -0.5, residual=tok)
-    old_w, old_kv = ops.XATTN_PACKED_W, ops.XATTN_PACKED_KV
-    outs = {}
-    try:
-        ops.XATTN_PACKED_W = True
-        for pkv in (False, True):
-            ops.XATTN_PACKED_KV = pkv
-            y = ops.cross_attention_block(tok, kv, pcq, pco, **kw)
-            yn, t3 = ops.cross_attention_block(tok, kv, pcq, pco, norm_in=(gg, bb, 1e-5), norm_out=(gg, bb, 1e-5), **kw)
-            torch.cuda.synchronize()
-            outs[pkv] = (y, yn, t3)
-    finally:
-        ops.XATTN_PACKED_W, ops.XATTN_PACKED_KV = old_w, old_kv
-    assert kv._xattn_kvp.shape == (B, C // D, 2, 80, D)
-    assert torch.equal(kv._xattn_kvp[:, :, 0, :nk], kv[:, :C].view(B, nk, C // D, D).permute(0, 2, 1, 3))
-    for a_, b_ in zip(outs[False], outs[True]):
-        assert torch.equal(a_, b_)
-
-
 def test_xattn_pack_weight_layout_and_rejects(ops, sdk):
     """The packed layout: piece ((nb * C/32 + ks) * 64 + lane) = W[16 nb + lane % 16, 32 ks + 8 (lane // 16) : +8];
     bad shapes / strides are refused."""

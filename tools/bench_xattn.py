@@ -169,10 +169,8 @@ def ab_arms(which):
     nk = 77
     if which == "waves640":
         arms, setter, reset, cw = (4, 8), lib().sdk_xattn_debug_waves640, 8, 640
-    elif which == "packed":
+    else:
         arms, setter, reset, cw = (0, 1), lambda v: setattr(ops, "XATTN_PACKED_W", bool(v)), 1, None
-    else:   # packedkv: the context K|V head-packed as well (weights packed in both arms)
-        arms, setter, reset, cw = (0, 1), lambda v: setattr(ops, "XATTN_PACKED_KV", bool(v)), 0, None
     for name, B, N, C, D in SHAPES:
         if (cw is not None and C != cw) or not ops.cross_attention_block_supported(C, D, nk, N):
             continue
@@ -208,7 +206,7 @@ def ab_arms(which):
 
 
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] in ("--waves640", "--packed", "--packedkv"):
+    if len(sys.argv) > 1 and sys.argv[1] in ("--waves640", "--packed"):
         ab_arms(sys.argv[1][2:])
     elif len(sys.argv) > 1 and sys.argv[1] == "--phases":
         phases()
